@@ -1,0 +1,362 @@
+"""go_raytracer_amd — MI355X-native drop-in for go_raytracer's render loop.
+
+Python face of the C ABI (include/rt_abi.h).  The object model mirrors the
+reference package API: ``Tree`` methods are the hittable constructors
+(NewSphere, NewQuad, NewBox, RotateY, Translate, ConstantMedium, BuildBVH, ...),
+``Camera`` mirrors camera.Camera's public fields (camera.go:26-36) with the
+same zero-means-default rules, and ``Camera.Render(world, lights)`` renders
+through the HIP path (camera.go:156).  There is no CPU render path here: the
+HIP library must be built and a GPU present, otherwise calls raise.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import (RT_NOISE_MARBLE, RT_NOISE_PERLIN, RT_NOISE_TURBULENT, RtCamera,  # noqa: F401
+                   RtCameraDerived, RtError, RtRenderOpts, RtSceneInfo, RtStats, RtTreeView,
+                   check, lib)
+
+__all__ = ["Tree", "Camera", "Scene", "quantize", "format_ppm", "device_count", "RtError",
+           "demo_scene", "DEMO_SCENES"]
+
+DEMO_SCENES = ("book1", "book2", "book3", "simple_light", "quads", "cornell", "cornell_smoke",
+               "model")
+
+
+def _d3(v):
+    return _lib.D3(*[float(x) for x in v])
+
+
+class Tree:
+    """A scene under construction (rt_tree).  Handles are plain ints."""
+
+    def __init__(self, seed=1):
+        p = C.c_void_p()
+        check(lib().rt_tree_create(C.byref(p)))
+        self._p = p
+        check(lib().rt_tree_seed(self._p, seed))
+
+    def __del__(self):
+        if getattr(self, "_p", None):
+            lib().rt_tree_destroy(self._p)
+            self._p = None
+
+    @property
+    def ptr(self):
+        return self._p
+
+    # scene RNG (replaces math/rand for scene content)
+    def rand(self):
+        return lib().rt_tree_rand(self._p)
+
+    def rand_range(self, lo, hi):
+        return lib().rt_tree_rand_range(self._p, lo, hi)
+
+    def randn(self, n):
+        return lib().rt_tree_randn(self._p, n)
+
+    # textures
+    def solid(self, r, g, b):
+        return check(lib().rt_tex_solid(self._p, r, g, b))
+
+    def checker(self, scale, even, odd):
+        return check(lib().rt_tex_checker(self._p, scale, even, odd))
+
+    def image(self, rgb):
+        a = np.ascontiguousarray(rgb, dtype=np.uint8)
+        h, w = a.shape[:2]
+        return check(lib().rt_tex_image(self._p, a.ctypes.data, w, h))
+
+    def noise(self, scale, variant=RT_NOISE_PERLIN):
+        return check(lib().rt_tex_noise(self._p, scale, variant))
+
+    def noise_tables(self, scale, variant, ranvec, perm):
+        rv = np.ascontiguousarray(ranvec, dtype=np.float64).reshape(256, 3)
+        pm = np.ascontiguousarray(perm, dtype=np.int32).reshape(3, 256)
+        return check(lib().rt_tex_noise_tables(
+            self._p, scale, variant, rv.ctypes.data_as(C.POINTER(C.c_double)),
+            pm.ctypes.data_as(C.POINTER(C.c_int32))))
+
+    # materials (a colour tuple means NewLambertian / NewDiffuseLight / NewIsotropic)
+    def _tex(self, t):
+        return t if isinstance(t, int) else self.solid(*t)
+
+    def lambertian(self, tex):
+        return check(lib().rt_mat_lambertian(self._p, self._tex(tex)))
+
+    def metal(self, albedo, fuzz):
+        return check(lib().rt_mat_metal(self._p, *[float(x) for x in albedo], fuzz))
+
+    def dielectric(self, ior):
+        return check(lib().rt_mat_dielectric(self._p, ior))
+
+    def light(self, tex):
+        return check(lib().rt_mat_diffuse_light(self._p, self._tex(tex)))
+
+    def isotropic(self, tex):
+        return check(lib().rt_mat_isotropic(self._p, self._tex(tex)))
+
+    # hittables
+    def list(self, *objs):
+        h = check(lib().rt_new_list(self._p))
+        for o in objs:
+            self.add(h, o)
+        return h
+
+    def add(self, lst, obj):
+        check(lib().rt_list_add(self._p, lst, obj))
+
+    def bvh(self, lst):
+        return check(lib().rt_build_bvh(self._p, lst))
+
+    def sphere(self, center, radius, mat):
+        return check(lib().rt_new_sphere(self._p, _d3(center), radius, mat))
+
+    def motion_sphere(self, c1, c2, radius, mat):
+        return check(lib().rt_new_motion_sphere(self._p, _d3(c1), _d3(c2), radius, mat))
+
+    def quad(self, Q, u, v, mat):
+        return check(lib().rt_new_quad(self._p, _d3(Q), _d3(u), _d3(v), mat))
+
+    def box(self, a, b, mat):
+        return check(lib().rt_new_box(self._p, _d3(a), _d3(b), mat))
+
+    def triangle(self, verts, mat, normals=None, uv=None):
+        v = np.ascontiguousarray(verts, dtype=np.float64).reshape(9)
+        n = None if normals is None else np.ascontiguousarray(normals, dtype=np.float64).reshape(9)
+        t = None if uv is None else np.ascontiguousarray(uv, dtype=np.float64).reshape(6)
+        dp = C.POINTER(C.c_double)
+        return check(lib().rt_new_triangle(
+            self._p, v.ctypes.data_as(dp), None if n is None else n.ctypes.data_as(dp),
+            None if t is None else t.ctypes.data_as(dp), mat))
+
+    def triangles(self, verts, mats, normals=None, uv=None):
+        v = np.ascontiguousarray(verts, dtype=np.float64).reshape(-1, 9)
+        n_tri = v.shape[0]
+        m = np.ascontiguousarray(np.broadcast_to(np.asarray(mats, dtype=np.int32), (n_tri,)))
+        dp = C.POINTER(C.c_double)
+        n = None if normals is None else np.ascontiguousarray(normals, dtype=np.float64).reshape(-1, 9)
+        t = None if uv is None else np.ascontiguousarray(uv, dtype=np.float64).reshape(-1, 6)
+        return check(lib().rt_new_triangles(
+            self._p, n_tri, v.ctypes.data_as(dp), None if n is None else n.ctypes.data_as(dp),
+            None if t is None else t.ctypes.data_as(dp), m.ctypes.data_as(C.POINTER(C.c_int32))))
+
+    def translate(self, obj, offset):
+        return check(lib().rt_translate(self._p, obj, _d3(offset)))
+
+    def rotate_y(self, obj, degrees):
+        return check(lib().rt_rotate_y(self._p, obj, degrees))
+
+    def medium(self, boundary, density, tex):
+        return check(lib().rt_constant_medium(self._p, boundary, density, self._tex(tex)))
+
+    def view(self):
+        v = RtTreeView()
+        check(lib().rt_tree_get_view(self._p, C.byref(v)))
+        return v
+
+
+class Camera:
+    """camera.Camera (camera.go:24-62): public fields, 0 means default."""
+
+    _FIELDS = ("AspectRatio", "Width", "SamplesPerPixel", "MaxDepth", "MaxThreads", "VerticalFOV",
+               "DefocusAngle", "FocusDistance", "Background", "MaxContribution")
+
+    def __init__(self, **kw):
+        self.AspectRatio = 0.0
+        self.Width = 0
+        self.SamplesPerPixel = 0
+        self.MaxDepth = 0
+        self.MaxThreads = 0
+        self.VerticalFOV = 0.0
+        self.DefocusAngle = 0.0
+        self.FocusDistance = 0.0
+        self.Background = (0.0, 0.0, 0.0)
+        self.MaxContribution = 0.0
+        self._pos = None
+        for k, v in kw.items():
+            if k not in self._FIELDS:
+                raise AttributeError(k)
+            setattr(self, k, v)
+
+    def PositionCamera(self, lookFrom=None, lookAt=None, vup=None):  # camera.go:65-81
+        self._pos = (tuple(lookFrom) if lookFrom is not None else (0.0, 0.0, 0.0),
+                     tuple(lookAt) if lookAt is not None else (0.0, 0.0, -1.0),
+                     tuple(vup) if vup is not None else (0.0, 1.0, 0.0))
+
+    def to_c(self):
+        c = RtCamera()
+        c.aspect_ratio = self.AspectRatio
+        c.width = int(self.Width)
+        c.samples_per_pixel = int(self.SamplesPerPixel)
+        c.max_depth = int(self.MaxDepth)
+        c.max_threads = int(self.MaxThreads)
+        c.vertical_fov = self.VerticalFOV
+        c.defocus_angle = self.DefocusAngle
+        c.focus_distance = self.FocusDistance
+        c.background = _d3(self.Background)
+        c.max_contribution = self.MaxContribution
+        if self._pos is not None:
+            c.positioned = 1
+            c.look_from, c.look_at, c.vup = (_d3(x) for x in self._pos)
+        return c
+
+    @classmethod
+    def from_c(cls, c):
+        cam = cls()
+        cam.AspectRatio = c.aspect_ratio
+        cam.Width = c.width
+        cam.SamplesPerPixel = c.samples_per_pixel
+        cam.MaxDepth = c.max_depth
+        cam.MaxThreads = c.max_threads
+        cam.VerticalFOV = c.vertical_fov
+        cam.DefocusAngle = c.defocus_angle
+        cam.FocusDistance = c.focus_distance
+        cam.Background = tuple(c.background)
+        cam.MaxContribution = c.max_contribution
+        if c.positioned:
+            cam._pos = (tuple(c.look_from), tuple(c.look_at), tuple(c.vup))
+        return cam
+
+    def derived(self):
+        d = RtCameraDerived()
+        c = self.to_c()
+        check(lib().rt_camera_derive(C.byref(c), C.byref(d)))
+        return d
+
+    def image_size(self):
+        d = self.derived()
+        return d.width, d.height, d.spp_sqrt
+
+    def Render(self, tree, world, lights, seed=1, device=0):
+        """Render the full image on one GPU -> float32 [H, W, 3] linear mean RGB."""
+        with Scene(tree, world, lights) as sc:
+            img, _ = sc.render(self, seed=seed, device=device)
+        return img
+
+
+class Scene:
+    """A flattened scene (rt_scene): BVH built on the host, uploaded on first render."""
+
+    def __init__(self, tree, world, lights=-1):
+        p = C.c_void_p()
+        check(lib().rt_scene_create(tree.ptr, world, lights, C.byref(p)))
+        self._p = p
+        self.tree = tree
+
+    def close(self):
+        if getattr(self, "_p", None):
+            lib().rt_scene_destroy(self._p)
+            self._p = None
+
+    __del__ = close
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def info(self):
+        i = RtSceneInfo()
+        check(lib().rt_scene_info_get(self._p, C.byref(i)))
+        return {f: getattr(i, f) for f, _ in RtSceneInfo._fields_}
+
+    def export_bvh(self):
+        nn, nr, root = C.c_int32(), C.c_int32(), C.c_uint32()
+        check(lib().rt_scene_export_bvh(self._p, None, C.byref(nn), None, C.byref(nr), C.byref(root)))
+        nodes = np.zeros((max(nn.value, 0), 16), np.float32)
+        refs = np.zeros(max(nr.value, 0), np.uint32)
+        check(lib().rt_scene_export_bvh(self._p, nodes.ctypes.data or None, C.byref(nn),
+                                        refs.ctypes.data or None, C.byref(nr), C.byref(root)))
+        n = C.c_int32()
+        check(lib().rt_scene_export_prim_bounds(self._p, None, C.byref(n)))
+        bounds = np.zeros((n.value, 6), np.float32)
+        check(lib().rt_scene_export_prim_bounds(self._p, bounds.ctypes.data or None, C.byref(n)))
+        return nodes, refs, int(root.value), bounds
+
+    @staticmethod
+    def _opts(seed, device, rank, nranks, path_slots, chunk, profile, stream):
+        o = RtRenderOpts()
+        o.seed = seed
+        o.device = device
+        o.rank = rank
+        o.nranks = nranks
+        o.path_slots = path_slots
+        o.chunk = chunk
+        o.flags = _lib.RT_FLAG_PROFILE if profile else 0
+        o.stream = stream
+        return o
+
+    def render(self, camera, seed=1, device=0, rank=0, nranks=1, path_slots=0, chunk=0,
+               profile=False, trace=None):
+        """Render this rank's rows -> (float32 [rows, W, 3], stats dict).
+
+        trace=(pixel, sample) additionally returns stats["trace"]: float32 [V, 12]
+        {o.xyz, time, d.xyz, vertex, t, u, v, ref bits} per world.Hit of that sample.
+        """
+        d = camera.derived()
+        rows = len(range(rank, d.height, nranks))
+        out = np.zeros((rows, d.width, 3), np.float32)
+        st = RtStats()
+        c = camera.to_c()
+        o = self._opts(seed, device, rank, nranks, path_slots, chunk, profile, None)
+        tbuf = None
+        if trace is not None:
+            tbuf = np.zeros((d.max_depth + 1, 12), np.float32)
+            o.trace_pixel, o.trace_sample = int(trace[0]), int(trace[1])
+            o.trace_cap = tbuf.shape[0]
+            o.trace_out = tbuf.ctypes.data
+        check(lib().rt_render(self._p, C.byref(c), C.byref(o), out.ctypes.data, C.byref(st)))
+        res = {f: getattr(st, f) for f, _ in RtStats._fields_}
+        if tbuf is not None:
+            res["trace"] = tbuf[tbuf[:, 7] >= 0]
+        return out, res
+
+    def render_device(self, camera, out_ptr, seed=1, device=0, rank=0, nranks=1, path_slots=0,
+                      chunk=0, profile=False, stream=None):
+        """Render into a device buffer (e.g. torch tensor .data_ptr()) on `stream`."""
+        st = RtStats()
+        c = camera.to_c()
+        o = self._opts(seed, device, rank, nranks, path_slots, chunk, profile, stream)
+        check(lib().rt_render_device(self._p, C.byref(c), C.byref(o), C.c_void_p(out_ptr),
+                                     C.byref(st)))
+        return {f: getattr(st, f) for f, _ in RtStats._fields_}
+
+
+def demo_scene(name, seed=1, asset_dir=None):
+    """Build a main.go scene -> (tree, camera, world, lights)."""
+    import os
+    if asset_dir is None:
+        asset_dir = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                 "assets")
+    t = Tree(seed)
+    cam = RtCamera()
+    w, l = C.c_int(), C.c_int()
+    check(lib().rt_demo_scene(t.ptr, name.encode(), asset_dir.encode(), C.byref(cam), C.byref(w),
+                              C.byref(l)))
+    return t, Camera.from_c(cam), w.value, l.value
+
+
+def quantize(rgb):
+    """PrintColor (vec/color.go:23-46) on a float32 [..., 3] image -> uint8."""
+    a = np.ascontiguousarray(rgb, dtype=np.float32)
+    out = np.zeros(a.shape, np.uint8)
+    check(lib().rt_quantize(a.ctypes.data, a.size // 3, out.ctypes.data))
+    return out
+
+
+def format_ppm(rgb):
+    """PPM P3 text exactly as the reference writes it (camera.go:160 + PrintColor)."""
+    a = np.ascontiguousarray(rgb, dtype=np.float32)
+    h, w = a.shape[:2]
+    n = lib().rt_format_ppm(a.ctypes.data, w, h, None, 0)
+    check(int(n))
+    buf = C.create_string_buffer(int(n))
+    check(int(lib().rt_format_ppm(a.ctypes.data, w, h, buf, n)))
+    return buf.raw[:n]
+
+
+def device_count():
+    return lib().rt_device_count()

@@ -1,0 +1,241 @@
+// host_bvh.cpp — the device BVH: binned-SAH BVH2, nodes in BFS order so the top
+// of the tree is one contiguous block that the extend kernel stages in LDS.
+//
+// The reference builds a median-split binary tree over interface values and
+// visits both children of every node, left first (bvh.go:21-82).  The closest
+// hit does not depend on the topology (ties aside), so the device tree is our
+// own: SAH splits, leaves of up to 4 prims, near-child-first traversal.
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <deque>
+
+#include "rt_internal.h"
+
+namespace rt {
+namespace {
+
+struct Box {
+  float mn[3] = {INFINITY, INFINITY, INFINITY};
+  float mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  void grow(const Box& b) {
+    for (int i = 0; i < 3; ++i) {
+      mn[i] = std::min(mn[i], b.mn[i]);
+      mx[i] = std::max(mx[i], b.mx[i]);
+    }
+  }
+  void grow_pt(const float* p) {
+    for (int i = 0; i < 3; ++i) {
+      mn[i] = std::min(mn[i], p[i]);
+      mx[i] = std::max(mx[i], p[i]);
+    }
+  }
+  double area() const {
+    double d[3];
+    for (int i = 0; i < 3; ++i) d[i] = std::max(0.0, (double)mx[i] - (double)mn[i]);
+    return 2.0 * (d[0] * d[1] + d[1] * d[2] + d[2] * d[0]);
+  }
+};
+
+struct TmpNode {
+  Box box;
+  int first = 0, count = 0;  // prim range (leaf)
+  int left = -1, right = -1; // children (inner)
+  int depth = 0;
+};
+
+constexpr int kBins = 16;
+constexpr int kLeafTarget = 4;  // SAH may stop at <= 4 prims
+constexpr double kCostTrav = 1.0, kCostIsect = 1.0;
+
+}  // namespace
+
+int build_bvh(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi,
+              const std::vector<uint32_t>& prims) {
+  const int n = (int)prims.size();
+  s.nodes.clear();
+  s.refs.clear();
+  s.prim_bounds.clear();
+  s.bvh_depth = 0;
+  s.max_leaf = 0;
+  if (n == 0) {
+    s.root = PRIM_NONE;
+    return RT_OK;
+  }
+  if ((uint32_t)n > 0x7FFFFFFu) return set_error(RT_ERR_UNSUPPORTED, "too many prims (%d)", n);
+
+  std::vector<Box> pb(n);
+  std::vector<float> cen(3 * (size_t)n);
+  for (int i = 0; i < n; ++i) {
+    pb[i].mn[0] = lo[i].x;
+    pb[i].mn[1] = lo[i].y;
+    pb[i].mn[2] = lo[i].z;
+    pb[i].mx[0] = hi[i].x;
+    pb[i].mx[1] = hi[i].y;
+    pb[i].mx[2] = hi[i].z;
+    for (int a = 0; a < 3; ++a) cen[3 * (size_t)i + a] = 0.5f * (pb[i].mn[a] + pb[i].mx[a]);
+  }
+  std::vector<int> idx(n);
+  for (int i = 0; i < n; ++i) idx[i] = i;
+
+  std::vector<TmpNode> tn;
+  tn.reserve(2 * (size_t)n / kLeafTarget + 16);
+  tn.push_back(TmpNode());
+  tn[0].first = 0;
+  tn[0].count = n;
+  std::vector<int> work = {0};
+  while (!work.empty()) {
+    int ni = work.back();
+    work.pop_back();
+    TmpNode& nd = tn[ni];
+    Box bb, cb;
+    for (int i = nd.first; i < nd.first + nd.count; ++i) {
+      bb.grow(pb[idx[i]]);
+      cb.grow_pt(&cen[3 * (size_t)idx[i]]);
+    }
+    nd.box = bb;
+    s.bvh_depth = std::max(s.bvh_depth, nd.depth);
+    if (nd.count <= 1) continue;
+
+    // binned SAH over all three axes
+    double best_cost = INFINITY;
+    int best_axis = -1, best_split = -1;
+    for (int a = 0; a < 3; ++a) {
+      float ext = cb.mx[a] - cb.mn[a];
+      if (!(ext > 0)) continue;
+      Box bins[kBins];
+      int cnt[kBins] = {0};
+      float k = kBins / ext;
+      for (int i = nd.first; i < nd.first + nd.count; ++i) {
+        int b = (int)((cen[3 * (size_t)idx[i] + a] - cb.mn[a]) * k);
+        b = std::min(std::max(b, 0), kBins - 1);
+        cnt[b]++;
+        bins[b].grow(pb[idx[i]]);
+      }
+      double left_area[kBins];
+      int left_cnt[kBins];
+      Box acc;
+      int c = 0;
+      for (int b = 0; b < kBins - 1; ++b) {
+        acc.grow(bins[b]);
+        c += cnt[b];
+        left_area[b] = acc.area();
+        left_cnt[b] = c;
+      }
+      acc = Box();
+      c = 0;
+      for (int b = kBins - 1; b > 0; --b) {
+        acc.grow(bins[b]);
+        c += cnt[b];
+        int lc = left_cnt[b - 1];
+        if (lc == 0 || c == 0) continue;
+        double cost = left_area[b - 1] * lc + acc.area() * c;
+        if (cost < best_cost) {
+          best_cost = cost;
+          best_axis = a;
+          best_split = b;
+        }
+      }
+    }
+    double parent_area = std::max(bb.area(), 1e-30);
+    double split_cost = kCostTrav + kCostIsect * best_cost / parent_area;
+    double leaf_cost = kCostIsect * nd.count;
+    int mid;
+    if (best_axis >= 0 && !(nd.count <= kLeafTarget && leaf_cost <= split_cost)) {
+      float ext = cb.mx[best_axis] - cb.mn[best_axis];
+      float k = kBins / ext;
+      auto it = std::partition(idx.begin() + nd.first, idx.begin() + nd.first + nd.count, [&](int p) {
+        int b = (int)((cen[3 * (size_t)p + best_axis] - cb.mn[best_axis]) * k);
+        b = std::min(std::max(b, 0), kBins - 1);
+        return b < best_split;
+      });
+      mid = (int)(it - idx.begin());
+    } else if (nd.count <= kLeafTarget) {
+      continue;  // leaf
+    } else {
+      // no usable SAH split (coincident centroids): median split by index
+      if (nd.count <= MAX_LEAF && best_axis < 0) continue;
+      int a = 0;
+      float e = -1;
+      for (int q = 0; q < 3; ++q)
+        if (cb.mx[q] - cb.mn[q] > e) {
+          e = cb.mx[q] - cb.mn[q];
+          a = q;
+        }
+      mid = nd.first + nd.count / 2;
+      std::nth_element(idx.begin() + nd.first, idx.begin() + mid, idx.begin() + nd.first + nd.count,
+                       [&](int p, int q) { return cen[3 * (size_t)p + a] < cen[3 * (size_t)q + a]; });
+    }
+    if (mid == nd.first || mid == nd.first + nd.count) mid = nd.first + nd.count / 2;
+    TmpNode L, R;
+    L.first = nd.first;
+    L.count = mid - nd.first;
+    R.first = mid;
+    R.count = nd.first + nd.count - mid;
+    L.depth = R.depth = nd.depth + 1;
+    int li = (int)tn.size();
+    tn.push_back(L);
+    tn.push_back(R);
+    tn[ni].left = li;
+    tn[ni].right = li + 1;
+    work.push_back(li + 1);
+    work.push_back(li);
+  }
+
+  // permuted refs + bounds
+  s.refs.resize(n);
+  s.prim_bounds.resize(6 * (size_t)n);
+  for (int i = 0; i < n; ++i) {
+    s.refs[i] = prims[idx[i]];
+    for (int a = 0; a < 3; ++a) {
+      s.prim_bounds[6 * (size_t)i + a] = pb[idx[i]].mn[a];
+      s.prim_bounds[6 * (size_t)i + 3 + a] = pb[idx[i]].mx[a];
+    }
+  }
+  auto leaf_of = [&](const TmpNode& x) -> uint32_t {
+    s.max_leaf = std::max(s.max_leaf, x.count);
+    return leaf_code((uint32_t)x.first, (uint32_t)x.count);
+  };
+  for (const auto& x : tn)
+    if (x.left < 0 && x.count > MAX_LEAF)
+      return set_error(RT_ERR_UNSUPPORTED, "BVH leaf of %d prims exceeds %d", x.count, MAX_LEAF);
+
+  if (tn[0].left < 0) {
+    s.root = leaf_of(tn[0]);
+    return RT_OK;
+  }
+  // BFS numbering of inner nodes
+  std::vector<int> order;
+  std::vector<int> out_index(tn.size(), -1);
+  std::deque<int> q = {0};
+  while (!q.empty()) {
+    int i = q.front();
+    q.pop_front();
+    out_index[i] = (int)order.size();
+    order.push_back(i);
+    for (int c : {tn[i].left, tn[i].right})
+      if (tn[c].left >= 0) q.push_back(c);
+  }
+  s.nodes.assign(4 * order.size(), F4{0, 0, 0, 0});
+  auto bits = [](uint32_t u) {
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+  };
+  for (size_t o = 0; o < order.size(); ++o) {
+    const TmpNode& nd = tn[order[o]];
+    const TmpNode& a = tn[nd.left];
+    const TmpNode& b = tn[nd.right];
+    uint32_t ca = a.left >= 0 ? (uint32_t)out_index[nd.left] : leaf_of(a);
+    uint32_t cbits = b.left >= 0 ? (uint32_t)out_index[nd.right] : leaf_of(b);
+    s.nodes[4 * o + 0] = {a.box.mn[0], a.box.mn[1], a.box.mn[2], bits(ca)};
+    s.nodes[4 * o + 1] = {a.box.mx[0], a.box.mx[1], a.box.mx[2], bits(cbits)};
+    s.nodes[4 * o + 2] = {b.box.mn[0], b.box.mn[1], b.box.mn[2], 0};
+    s.nodes[4 * o + 3] = {b.box.mx[0], b.box.mx[1], b.box.mx[2], 0};
+  }
+  s.root = 0;
+  return RT_OK;
+}
+
+}  // namespace rt

@@ -1,0 +1,82 @@
+// host_scene.cpp — rt_scene_create / info / export (host side, no GPU needed).
+#include <string.h>
+
+#include "rt_internal.h"
+
+using rt::set_error;
+
+extern "C" {
+
+int rt_scene_create(const rt_tree* t, int world, int lights, rt_scene** out) {
+  if (!t || !out) return set_error(RT_ERR_INVALID, "rt_scene_create: null");
+  *out = nullptr;
+  rt_scene* s = new (std::nothrow) rt_scene();
+  if (!s) return set_error(RT_ERR_OOM, "rt_scene_create: out of memory");
+  int rc = rt::flatten_scene(t->t, world, lights, s->s.h);
+  if (rc) {
+    delete s;
+    return rc;
+  }
+  *out = s;
+  return RT_OK;
+}
+
+int rt_scene_destroy(rt_scene* s) {
+  if (!s) return RT_OK;
+  rt::release_device(&s->s);
+  delete s;
+  return RT_OK;
+}
+
+int rt_scene_info_get(const rt_scene* sc, rt_scene_info* o) {
+  if (!sc || !o) return set_error(RT_ERR_INVALID, "rt_scene_info_get: null");
+  const rt::HostScene& h = sc->s.h;
+  memset(o, 0, sizeof *o);
+  o->n_spheres = (int32_t)h.sph_cr.size();
+  o->n_quads = (int32_t)(h.quad.size() / 5);
+  o->n_triangles = (int32_t)(h.tri.size() / 3);
+  o->n_world_prims = h.n_world_prims;
+  o->n_media = (int32_t)h.media.size();
+  o->n_lights = (int32_t)h.lights.size();
+  o->n_bvh_nodes = (int32_t)(h.nodes.size() / 4);
+  o->bvh_depth = h.bvh_depth;
+  o->max_leaf = h.max_leaf;
+  o->n_materials = (int32_t)h.mats.size();
+  o->n_textures = (int32_t)h.texs.size();
+  o->n_images = (int32_t)h.images.size();
+  o->n_perlins = (int32_t)h.perlins.size();
+  o->medium_draws = h.medium_draws;
+  int64_t b = 0;
+  b += h.sph_cr.size() * 16 + h.sph_mv.size() * 16 + h.sph_uv.size() * 8;
+  b += h.quad.size() * 16 + h.tri.size() * 16 + h.tri_attr.size() * 16;
+  b += h.nodes.size() * 16 + h.refs.size() * 4;
+  b += h.media.size() * sizeof(rt::DevMedium) + h.medium_refs.size() * 4;
+  b += h.lights.size() * sizeof(rt::DevLight) + h.mats.size() * sizeof(rt::DevMaterial);
+  b += h.texs.size() * sizeof(rt::DevTexture) + h.texels.size();
+  b += h.images.size() * sizeof(rt::DevImage) + h.perlins.size() * sizeof(rt::DevPerlin);
+  o->device_bytes = b;
+  return RT_OK;
+}
+
+int rt_scene_export_bvh(const rt_scene* sc, float* nodes, int32_t* n_nodes, uint32_t* prim_refs,
+                        int32_t* n_refs, uint32_t* root) {
+  if (!sc) return set_error(RT_ERR_INVALID, "rt_scene_export_bvh: null");
+  const rt::HostScene& h = sc->s.h;
+  if (n_nodes) *n_nodes = (int32_t)(h.nodes.size() / 4);
+  if (n_refs) *n_refs = (int32_t)h.refs.size();
+  if (root) *root = h.root;
+  if (nodes && !h.nodes.empty()) memcpy(nodes, h.nodes.data(), h.nodes.size() * 16);
+  if (prim_refs && !h.refs.empty()) memcpy(prim_refs, h.refs.data(), h.refs.size() * 4);
+  return RT_OK;
+}
+
+int rt_scene_export_prim_bounds(const rt_scene* sc, float* bounds, int32_t* n) {
+  if (!sc) return set_error(RT_ERR_INVALID, "rt_scene_export_prim_bounds: null");
+  const rt::HostScene& h = sc->s.h;
+  if (n) *n = (int32_t)(h.prim_bounds.size() / 6);
+  if (bounds && !h.prim_bounds.empty())
+    memcpy(bounds, h.prim_bounds.data(), h.prim_bounds.size() * 4);
+  return RT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,108 @@
+// rt_device.h — HBM layout of a flattened scene and of the wavefront path state.
+// Shared by the host flattener (g++) and the HIP kernels (hipcc).  POD only.
+//
+// Flattening (host_flatten.cpp) bakes Translate/RotateY (transformation.go) into
+// world-space primitives, separates constant media (medium.go) from the
+// closest-hit BVH, and turns the lights Hittable (hittable.go:89-103) into a
+// weighted table.  See DESIGN.md "Data layout in HBM".
+#pragma once
+#include <stdint.h>
+
+namespace rt {
+
+struct alignas(16) F4 {
+  float x, y, z, w;
+};
+struct alignas(8) F2 {
+  float x, y;
+};
+
+// ---- primitive references ------------------------------------------------
+// prim ref = (type << 30) | index
+enum : uint32_t { PRIM_SPHERE = 0u, PRIM_QUAD = 1u, PRIM_TRI = 2u, PRIM_MEDIUM = 3u };
+constexpr uint32_t PRIM_NONE = 0xFFFFFFFFu;
+inline constexpr uint32_t prim_ref(uint32_t type, uint32_t idx) { return (type << 30) | idx; }
+
+// ---- BVH2 node: both children's boxes stored in the parent (64 B) --------
+//  f4[0] = b0min.xyz | child0 bits      f4[1] = b0max.xyz | child1 bits
+//  f4[2] = b1min.xyz | 0                f4[3] = b1max.xyz | 0
+// child bits: bit31 set  -> leaf: first ref = (c >> 4) & 0x7FFFFFF, count = (c & 15) + 1
+//             bit31 clear-> inner node index
+constexpr uint32_t LEAF_BIT = 0x80000000u;
+constexpr int MAX_LEAF = 16;
+inline constexpr uint32_t leaf_code(uint32_t first, uint32_t count) {
+  return LEAF_BIT | (first << 4) | (count - 1u);
+}
+
+// ---- per-type primitive records ------------------------------------------
+// sphere (objects.go:14-37): sph_cr = center@t0 | radius ; sph_mv = motion | mat bits
+//   sph_uv = cos,sin of the baked Y rotation (UV is computed in object space, objects.go:113)
+// quad (objects.go:117-140): 5 x F4 = Q|D, u|area, v|mat, n|0, w|0
+// triangle (objects.go:242-316): hot 3 x F4 = v0|mat, e0|area, e1|flags
+//   attr 6 x F4 = face normal, vn0, vn1, vn2, (uv0,uv1), (uv2,0,0)
+enum : uint32_t { TRI_HAS_NORMALS = 1u, TRI_HAS_UV = 2u };
+
+struct DevMedium {           // constantMedium medium.go:13-18
+  uint32_t bfirst, bcount;   // boundary prim refs in medium_refs
+  float neg_inv_density;     // -1/rho
+  int32_t phase_mat;         // isotropic material
+  int32_t draw_base;         // first free-flight draw index for this occurrence
+  int32_t mult;              // free-flight draws (BVH span-1 leaf duplication, bvh.go:44-46)
+  int32_t _pad[2];
+};
+
+struct DevLight {            // one leaf of the lights Hittable
+  uint32_t ref;              // prim ref, PRIM_NONE for an empty HittableList
+  uint32_t lo24;             // pick interval lower bound (24-bit uniform)
+  float weight;              // product of 1/len along the list nesting
+  float _pad;
+};
+
+struct DevMaterial {         // materials.go
+  int32_t kind, tex;
+  float param;               // metal fuzz / dielectric ior
+  float _pad;
+  F4 albedo;                 // metal albedo
+};
+
+struct DevTexture {          // texture.go
+  int32_t kind, a, b, variant;
+  F4 color;                  // solid colour; .w = scale (checker inv_scale / noise scale)
+};
+
+struct DevImage {
+  uint64_t offset;           // into texels
+  int32_t w, h;
+};
+
+struct DevPerlin {           // perlin.go:10-31
+  F4 ranvec[256];
+  int32_t perm[3][256];
+};
+
+struct DevScene {
+  const F4* sph_cr;
+  const F4* sph_mv;
+  const F2* sph_uv;
+  const F4* quad;
+  const F4* tri;
+  const F4* tri_attr;
+  const F4* nodes;
+  const uint32_t* refs;
+  uint32_t root;
+  int32_t n_nodes;
+  const DevMedium* media;
+  const uint32_t* medium_refs;
+  int32_t n_media;
+  int32_t medium_draws;
+  const DevLight* lights;
+  int32_t n_lights;
+  int32_t _pad0;
+  const DevMaterial* mats;
+  const DevTexture* texs;
+  const uint8_t* texels;
+  const DevImage* images;
+  const DevPerlin* perlins;
+};
+
+}  // namespace rt

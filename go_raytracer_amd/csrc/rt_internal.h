@@ -1,0 +1,89 @@
+// rt_internal.h — host-side structures behind the opaque rt_tree / rt_scene handles.
+#pragma once
+#include <stdint.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "rt_abi.h"
+#include "rt_device.h"
+
+namespace rt {
+
+// thread-local error slot (rt_last_error)
+int set_error(int code, const char* fmt, ...);
+
+struct Tree {
+  // nodes as created; LIST/BVH children live in lists[node.a]
+  std::vector<rt_node> nodes;
+  std::vector<std::vector<int32_t>> lists;
+  std::vector<rt_tri> tris;
+  std::vector<rt_material> materials;
+  std::vector<rt_texture> textures;
+  std::vector<std::vector<uint8_t>> image_data;
+  std::vector<rt_image> images;
+  std::vector<rt_perlin> perlins;
+  uint64_t rng = 0x853c49e6748fea9bull;
+
+  // packed view (rebuilt lazily when dirty)
+  bool dirty = true;
+  std::vector<rt_node> v_nodes;
+  std::vector<int32_t> v_children;
+
+  double rand01();
+  int randn(int n);
+  void pack();
+};
+
+// Host copy of the flattened scene plus its device mirror.
+struct HostScene {
+  std::vector<F4> sph_cr, sph_mv;
+  std::vector<F2> sph_uv;
+  std::vector<F4> quad;      // 5 per quad
+  std::vector<F4> tri;       // 3 per tri
+  std::vector<F4> tri_attr;  // 6 per tri
+  std::vector<F4> nodes;     // 4 per node
+  std::vector<uint32_t> refs;
+  uint32_t root = PRIM_NONE;
+  std::vector<float> prim_bounds;  // 6 per world ref (export/tests)
+  std::vector<DevMedium> media;
+  std::vector<uint32_t> medium_refs;
+  int32_t medium_draws = 0;
+  std::vector<DevLight> lights;
+  std::vector<DevMaterial> mats;
+  std::vector<DevTexture> texs;
+  std::vector<uint8_t> texels;
+  std::vector<DevImage> images;
+  std::vector<DevPerlin> perlins;
+  int32_t n_world_prims = 0;
+  int32_t bvh_depth = 0;
+  int32_t max_leaf = 0;
+};
+
+struct DeviceScene;  // defined in the HIP translation unit
+struct RenderState;
+
+struct Scene {
+  HostScene h;
+  int device = -1;
+  DeviceScene* dev = nullptr;     // uploaded lazily by rt_render
+  RenderState* state = nullptr;   // wavefront buffers, reused across renders
+};
+
+// host_flatten.cpp
+int flatten_scene(const Tree& t, int world, int lights, HostScene& out);
+// host_bvh.cpp
+int build_bvh(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi,
+              const std::vector<uint32_t>& prims);
+// rt_render.hip
+void release_device(Scene* s);
+
+}  // namespace rt
+
+struct rt_tree {
+  rt::Tree t;
+};
+struct rt_scene {
+  rt::Scene s;
+};

@@ -1,0 +1,197 @@
+// rt_kernels.h — device-side math, sampling and intersection for the MI355X path.
+// Each function cites the reference function it re-implements.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rt_device.h"
+#include "rt_rng.h"
+
+namespace rt {
+
+#define RT_D __device__ __forceinline__
+
+constexpr float kPi = 3.14159265358979323846f;
+constexpr float kInf = __builtin_huge_valf();
+
+struct f3 {
+  float x, y, z;
+};
+RT_D f3 mk3(float x, float y, float z) { return {x, y, z}; }
+RT_D f3 xyz(const F4& v) { return {v.x, v.y, v.z}; }
+RT_D f3 operator+(f3 a, f3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+RT_D f3 operator-(f3 a, f3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+RT_D f3 operator-(f3 a) { return {-a.x, -a.y, -a.z}; }
+RT_D f3 operator*(f3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+RT_D f3 operator*(f3 a, f3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
+RT_D float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+RT_D f3 cross(f3 a, f3 b) {
+  return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+RT_D float length(f3 a) { return sqrtf(dot(a, a)); }
+RT_D f3 unit(f3 a) { return a * (1.0f / length(a)); }  // UnitVector vec.go:125
+RT_D bool finite3(f3 a) { return isfinite(a.x) && isfinite(a.y) && isfinite(a.z); }
+
+RT_D uint32_t fbits(float f) { return __float_as_uint(f); }
+RT_D float bitsf(uint32_t u) { return __uint_as_float(u); }
+RT_D F4 ldg4(const F4* p) { return *p; }
+
+// ------------------------------------------------------------- sampling ----
+// Distribution-identical closed forms of the reference's rejection samplers.
+// RandomUnitVector vec.go:159-167 (uniform on the sphere)
+RT_D f3 uniform_sphere(float u0, float u1) {
+  float z = 1.0f - 2.0f * u0;
+  float r = sqrtf(fmaxf(0.0f, 1.0f - z * z));
+  float phi = 2.0f * kPi * u1;
+  return {r * cosf(phi), r * sinf(phi), z};
+}
+// RandomUnitDisk vec.go:149-156 (uniform in the disk)
+RT_D f3 uniform_disk(float u0, float u1) {
+  float r = sqrtf(u0);
+  float phi = 2.0f * kPi * u1;
+  return {r * cosf(phi), r * sinf(phi), 0.0f};
+}
+// RandomCosineDirection vec.go:177-186 (same formula)
+RT_D f3 cosine_direction(float r1, float r2) {
+  float phi = 2.0f * kPi * r1;
+  float s = sqrtf(r2);
+  return {cosf(phi) * s, sinf(phi) * s, sqrtf(1.0f - r2)};
+}
+
+// NewONB onb.go:13-25 — note the 0.9 test is on the un-normalised vector
+struct Onb {
+  f3 u, v, w;
+};
+RT_D Onb make_onb(f3 n) {
+  Onb o;
+  o.w = unit(n);
+  f3 a = fabsf(n.x) > 0.9f ? mk3(0, 1, 0) : mk3(1, 0, 0);
+  o.v = unit(cross(n, a));
+  o.u = unit(cross(n, o.v));
+  return o;
+}
+RT_D f3 onb_transform(const Onb& o, f3 v) { return o.u * v.x + o.v * v.y + o.w * v.z; }  // :38-43
+
+// Reflect / Refract vec.go:136-146
+RT_D f3 reflect(f3 v, f3 n) { return v - n * (dot(n, v) * 2.0f); }
+RT_D f3 refract(f3 v, f3 n, float eta) {
+  float c = fminf(dot(-v, n), 1.0f);
+  f3 perp = (v + n * c) * eta;
+  f3 par = n * (-sqrtf(fabsf(1.0f - dot(perp, perp))));
+  return perp + par;
+}
+
+// clampContribution camera.go:334-341
+RT_D f3 clamp_contribution(f3 c, float maxv) {
+  float intensity = c.x + c.y + c.z;
+  if (intensity > maxv) return c * (maxv / intensity);
+  return c;
+}
+
+// --------------------------------------------------------- intersection ----
+// sphere.Hit objects.go:83-115 — evaluated in fp64 (fp32 cancels in
+// |oc|^2 - r^2 for the R=1000 ground and R=5000 fog spheres).  Open interval.
+RT_D bool hit_sphere_d(const DevScene& sc, uint32_t i, f3 o, f3 d, float time, double tmin,
+                       double tmax, double& t_out) {
+  const F4 cr = sc.sph_cr[i];
+  const F4 mv = sc.sph_mv[i];
+  double cx = (double)cr.x + (double)time * (double)mv.x;
+  double cy = (double)cr.y + (double)time * (double)mv.y;
+  double cz = (double)cr.z + (double)time * (double)mv.z;
+  double ox = cx - (double)o.x, oy = cy - (double)o.y, oz = cz - (double)o.z;
+  double dx = d.x, dy = d.y, dz = d.z;
+  double a = dx * dx + dy * dy + dz * dz;
+  double h = dx * ox + dy * oy + dz * oz;
+  double r = cr.w;
+  double c = ox * ox + oy * oy + oz * oz - r * r;
+  double disc = h * h - a * c;
+  if (disc < 0) return false;
+  double sq = sqrt(disc);
+  double root = (h - sq) / a;
+  if (!(tmin < root && root < tmax)) {
+    root = (h + sq) / a;
+    if (!(tmin < root && root < tmax)) return false;
+  }
+  t_out = root;
+  return true;
+}
+RT_D bool hit_sphere(const DevScene& sc, uint32_t i, f3 o, f3 d, float time, float tmin,
+                     float tmax, float& t_out) {
+  double t;
+  if (!hit_sphere_d(sc, i, o, d, time, (double)tmin, (double)tmax, t)) return false;
+  t_out = (float)t;
+  return true;
+}
+
+// quad.Hit objects.go:167-196 + isInterior :198-206 — closed interval
+RT_D bool hit_quad(const DevScene& sc, uint32_t i, f3 o, f3 d, float tmin, float tmax,
+                   float& t_out, float& a_out, float& b_out) {
+  const F4* q = sc.quad + 5 * (size_t)i;
+  const F4 Qd = q[0], U = q[1], Vm = q[2], N = q[3], W = q[4];
+  f3 n = xyz(N);
+  float denom = dot(n, d);
+  if (fabsf(denom) < 1e-8f) return false;
+  float t = (Qd.w - dot(n, o)) / denom;
+  if (!(tmin <= t && t <= tmax)) return false;
+  f3 pp = (o + d * t) - xyz(Qd);
+  f3 w = xyz(W);
+  float alpha = dot(w, cross(pp, xyz(Vm)));
+  float beta = dot(w, cross(xyz(U), pp));
+  if (!(0.0f <= alpha && alpha <= 1.0f) || !(0.0f <= beta && beta <= 1.0f)) return false;
+  t_out = t;
+  a_out = alpha;
+  b_out = beta;
+  return true;
+}
+
+// Triangle.Hit objects.go:408-461 (Moller-Trumbore), comparisons kept verbatim
+RT_D bool hit_tri(const DevScene& sc, uint32_t i, f3 o, f3 d, float tmin, float tmax,
+                  float& t_out, float& u_out, float& v_out) {
+  const F4* tr = sc.tri + 3 * (size_t)i;
+  const F4 V0 = tr[0], E0 = tr[1], E1 = tr[2];
+  f3 e0 = xyz(E0), e1 = xyz(E1);
+  f3 pvec = cross(d, e1);
+  float det = dot(e0, pvec);
+  if (fabsf(det) < 1e-8f) return false;
+  float inv = 1.0f / det;
+  f3 tvec = o - xyz(V0);
+  float u = dot(tvec, pvec) * inv;
+  if (u < 0.0f || u > 1.0f) return false;
+  f3 qvec = cross(tvec, e0);
+  float v = dot(d, qvec) * inv;
+  if (v < 0.0f || (u + v) > 1.0f) return false;
+  float t = dot(e1, qvec) * inv;
+  if (t < tmin || t > tmax) return false;
+  t_out = t;
+  u_out = u;
+  v_out = v;
+  return true;
+}
+
+RT_D bool hit_prim(const DevScene& sc, uint32_t ref, f3 o, f3 d, float time, float tmin,
+                   float tmax, float& t, float& u, float& v) {
+  uint32_t type = ref >> 30, idx = ref & 0x3FFFFFFFu;
+  if (type == PRIM_SPHERE) {
+    u = v = 0.0f;
+    return hit_sphere(sc, idx, o, d, time, tmin, tmax, t);
+  }
+  if (type == PRIM_QUAD) return hit_quad(sc, idx, o, d, tmin, tmax, t, u, v);
+  return hit_tri(sc, idx, o, d, tmin, tmax, t, u, v);
+}
+
+// same, with fp64 interval bounds and result (medium boundaries: the reference
+// searches (t1 + 1e-4, inf) with |t1| up to ~1e4, below fp32 resolution)
+RT_D bool hit_prim_d(const DevScene& sc, uint32_t ref, f3 o, f3 d, float time, double tmin,
+                     double tmax, double& t) {
+  uint32_t type = ref >> 30, idx = ref & 0x3FFFFFFFu;
+  if (type == PRIM_SPHERE) return hit_sphere_d(sc, idx, o, d, time, tmin, tmax, t);
+  float tf, u, v;
+  bool h = type == PRIM_QUAD ? hit_quad(sc, idx, o, d, -kInf, kInf, tf, u, v)
+                             : hit_tri(sc, idx, o, d, -kInf, kInf, tf, u, v);
+  if (!h) return false;
+  t = (double)tf;
+  if (type == PRIM_QUAD) return tmin <= t && t <= tmax;  // Contains
+  return !(t < tmin || t > tmax);                        // Triangle.Hit :433
+}
+
+}  // namespace rt

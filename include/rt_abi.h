@@ -1,0 +1,310 @@
+/*
+ * rt_abi.h — C ABI of the MI355X path-tracing hot path (go_raytracer_amd).
+ *
+ * Drop-in boundary for the reference's per-pixel render loop
+ *     (*Camera).Render(world, lights hittable.Hittable)   internal/camera/camera.go:156
+ * The reference has no FFI; the seam is its Go interfaces (Hittable
+ * hittable.go:60-65, Material materials.go:19-27, Texture texture.go:10-12).
+ * A cgo shim walks the Go object tree with the rt_new_* /
+ * rt_mat_* / rt_tex_* constructors below — one call per Go constructor — and
+ * then calls rt_scene_create + rt_render instead of Camera.Render.
+ *
+ * Conventions: every function returns RT_OK (0) or a negative RT_ERR_* code,
+ * or a non-negative handle.  Nothing aborts the process (the reference calls
+ * log.Fatal, camera.go:188, hittable.go:70, imageLoader.go:32-36); the message
+ * of the last failure on the calling thread is in rt_last_error().
+ * All inputs are copied; callers may free them after the call returns.
+ */
+#ifndef RT_ABI_H
+#define RT_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+enum {
+  RT_OK = 0,
+  RT_ERR_INVALID = -1,     /* bad argument / handle */
+  RT_ERR_UNSUPPORTED = -2, /* e.g. a BVH or transform used as a light (hittable.go:69-72) */
+  RT_ERR_DEVICE = -3,      /* HIP runtime failure or no GPU */
+  RT_ERR_OOM = -4,
+  RT_ERR_IO = -5
+};
+
+const char* rt_last_error(void);
+int rt_abi_version(void);
+
+/* ------------------------------------------------------------------------ */
+/* Scene tree: one constructor per reference constructor.                    */
+/* ------------------------------------------------------------------------ */
+typedef struct rt_tree rt_tree;
+
+int rt_tree_create(rt_tree** out);
+int rt_tree_destroy(rt_tree* t);
+
+/* Scene-construction randomness (the reference uses the global math/rand for
+ * random scene content, main.go:38-75,107,155, and perlin tables,
+ * perlin.go:20-31).  A per-tree splitmix64 stream replaces it. */
+int rt_tree_seed(rt_tree* t, uint64_t seed);
+double rt_tree_rand(rt_tree* t);             /* rand.Float64()        */
+double rt_tree_rand_range(rt_tree* t, double lo, double hi); /* util.RangeRange utilities.go:12 */
+int rt_tree_randn(rt_tree* t, int n);        /* rand.Intn(n)          */
+
+/* textures — texture.go */
+enum { RT_TEX_SOLID = 0, RT_TEX_CHECKER = 1, RT_TEX_IMAGE = 2, RT_TEX_NOISE = 3 };
+enum { RT_NOISE_PERLIN = 1, RT_NOISE_MARBLE = 2, RT_NOISE_TURBULENT = 3 }; /* texture.go:88-95 */
+int rt_tex_solid(rt_tree* t, double r, double g, double b);                 /* NewSolidColor texture.go:18 */
+int rt_tex_checker(rt_tree* t, double scale, int even_tex, int odd_tex);    /* NewCheckerboard texture.go:37 */
+/* NewImageTexture texture.go:66 with the image already decoded to RGB8
+ * rows (RTImage.bdata layout imageLoader.go:52-62); w*h*3 bytes copied. */
+int rt_tex_image(rt_tree* t, const uint8_t* rgb, int w, int h);
+/* NewNoiseTextureWithType texture.go:108: perlin tables drawn from the tree RNG
+ * in NewPerlin's order (perlin.go:20-31, 81-90). */
+int rt_tex_noise(rt_tree* t, double scale, int variant);
+/* same, with explicit tables (ranvec[256][3] doubles, perm[3][256]) */
+int rt_tex_noise_tables(rt_tree* t, double scale, int variant, const double* ranvec,
+                        const int32_t* perm);
+
+/* materials — materials.go */
+enum {
+  RT_MAT_LAMBERTIAN = 0,
+  RT_MAT_METAL = 1,
+  RT_MAT_DIELECTRIC = 2,
+  RT_MAT_DIFFUSE_LIGHT = 3,
+  RT_MAT_ISOTROPIC = 4
+};
+int rt_mat_lambertian(rt_tree* t, int tex);                               /* NewTexturedLambertian :40 */
+int rt_mat_metal(rt_tree* t, double r, double g, double b, double fuzz); /* NewMetal :65 */
+int rt_mat_dielectric(rt_tree* t, double ior);                            /* NewDielectric :89 */
+int rt_mat_diffuse_light(rt_tree* t, int tex);                            /* NewDiffuseLightTextured :139 */
+int rt_mat_isotropic(rt_tree* t, int tex);                                /* NewIsotropicTexture :165 */
+
+/* hittables — hittable.go, bvh.go, objects.go, transformation.go, medium.go */
+enum {
+  RT_NODE_LIST = 0,
+  RT_NODE_BVH = 1,
+  RT_NODE_SPHERE = 2,
+  RT_NODE_QUAD = 3,
+  RT_NODE_TRIANGLE = 4,
+  RT_NODE_TRANSLATE = 5,
+  RT_NODE_ROTATE_Y = 6,
+  RT_NODE_MEDIUM = 7
+};
+int rt_new_list(rt_tree* t);                        /* NewHittableList hittable.go:84 */
+int rt_list_add(rt_tree* t, int list, int obj);     /* HittableList.Add hittable.go:113 */
+int rt_build_bvh(rt_tree* t, int list);             /* BuildBVH bvh.go:21 */
+int rt_new_sphere(rt_tree* t, const double center[3], double radius, int mat); /* objects.go:23 */
+int rt_new_motion_sphere(rt_tree* t, const double c1[3], const double c2[3], double radius,
+                         int mat);                  /* NewMotionSphere objects.go:30 */
+int rt_new_quad(rt_tree* t, const double Q[3], const double u[3], const double v[3],
+                int mat);                           /* NewQuad objects.go:129 */
+int rt_new_box(rt_tree* t, const double a[3], const double b[3], int mat); /* NewBox objects.go:208 */
+/* NewTriangle / NewTriangleWithNormals / NewTexturedTriangle[WithNormals]
+ * objects.go:257-316.  normals (9) and uv (6) may be NULL. */
+int rt_new_triangle(rt_tree* t, const double v[9], const double* normals, const double* uv,
+                    int mat);
+/* bulk form for meshes: n triangles, returns a LIST node holding them */
+int rt_new_triangles(rt_tree* t, int n, const double* v, const double* normals,
+                     const double* uv, const int32_t* mats);
+int rt_translate(rt_tree* t, int obj, const double offset[3]);  /* Translate transformation.go:20 */
+int rt_rotate_y(rt_tree* t, int obj, double degrees);           /* RotateY transformation.go:48 */
+int rt_constant_medium(rt_tree* t, int boundary, double density, int tex); /* medium.go:20 */
+
+/* ------------------------------------------------------------------------ */
+/* Read-only view of a tree (consumed by the CPU oracle and the cgo shim).  */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  int32_t kind;  /* RT_NODE_* */
+  int32_t mat;   /* material id (prims), phase material (medium) */
+  int32_t a, b;  /* LIST/BVH: children[a .. a+b); TRANSLATE/ROTATE_Y: a = child;
+                    MEDIUM: a = boundary; TRIANGLE: a = index into tris */
+  double p[10];  /* SPHERE: c1[3] c2[3] r moving; QUAD: Q u v; TRANSLATE: off;
+                    ROTATE_Y: degrees; MEDIUM: density */
+} rt_node;
+
+typedef struct {
+  double v[9];   /* 3 vertices */
+  double n[9];   /* vertex normals (if flags & 1) */
+  double uv[6];  /* texture coords (if flags & 2) */
+  int32_t flags; /* 1 = has vertex normals, 2 = has uv */
+  int32_t mat;
+} rt_tri;
+
+typedef struct {
+  int32_t kind;   /* RT_MAT_* */
+  int32_t tex;    /* lambertian / light / isotropic */
+  double albedo[3];
+  double fuzz;
+  double ior;
+} rt_material;
+
+typedef struct {
+  int32_t kind;    /* RT_TEX_* */
+  int32_t a, b;    /* CHECKER: even, odd; IMAGE: image id; NOISE: perlin id */
+  int32_t variant; /* NOISE */
+  double color[3]; /* SOLID */
+  double scale;    /* CHECKER: inv_scale (= 1/scale as texture.go:39); NOISE: scale */
+} rt_texture;
+
+typedef struct {
+  int32_t w, h;
+  const uint8_t* rgb; /* w*h*3 */
+} rt_image;
+
+typedef struct {
+  double ranvec[256][3];
+  int32_t perm[3][256];
+} rt_perlin;
+
+typedef struct {
+  const rt_node* nodes;
+  int32_t n_nodes;
+  const int32_t* children;
+  int32_t n_children;
+  const rt_tri* tris;
+  int32_t n_tris;
+  const rt_material* materials;
+  int32_t n_materials;
+  const rt_texture* textures;
+  int32_t n_textures;
+  const rt_image* images;
+  int32_t n_images;
+  const rt_perlin* perlins;
+  int32_t n_perlins;
+} rt_tree_view;
+
+int rt_tree_get_view(const rt_tree* t, rt_tree_view* out);
+
+/* ------------------------------------------------------------------------ */
+/* Camera — public fields of Camera camera.go:26-36 + PositionCamera :65.    */
+/* Zero means "use the reference default" exactly as initialize() :181-207. */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  double aspect_ratio;        /* 0 -> 1.0 */
+  int32_t width;              /* 0 -> 100 */
+  int32_t samples_per_pixel;  /* 0 -> 100 (truncated to floor(sqrt)^2, camera.go:211) */
+  int32_t max_depth;          /* 0 -> 10 */
+  int32_t max_threads;        /* -N; unused by the GPU path (kept for API parity) */
+  double vertical_fov;        /* 0 -> 90 */
+  double defocus_angle;       /* 0 -> 0 */
+  double focus_distance;      /* 0 -> 10 */
+  double background[3];       /* Background (nil in Go == black here) */
+  double max_contribution;    /* 0 -> 1.5 */
+  double look_from[3];        /* PositionCamera; a never-positioned camera uses */
+  double look_at[3];          /*   lookFrom (0,0,0), lookAt (0,0,-1), vup (0,1,0) */
+  double vup[3];
+  int32_t positioned;         /* 0 -> the defaults above */
+  int32_t _pad;
+} rt_camera;
+
+/* Derived geometry, initialize() camera.go:179-253 (fp64). */
+typedef struct {
+  int32_t width, height, spp_sqrt, max_depth;
+  double pixel_samples_scale, recip_spp_sqrt;
+  double center[3], pixel00[3], delta_u[3], delta_v[3], defocus_u[3], defocus_v[3];
+  double defocus_angle, max_contribution;
+  double background[3];
+} rt_camera_derived;
+
+int rt_camera_derive(const rt_camera* cam, rt_camera_derived* out);
+
+/* ------------------------------------------------------------------------ */
+/* Flattened scene + render.                                                 */
+/* ------------------------------------------------------------------------ */
+typedef struct rt_scene rt_scene;
+
+/* Flatten world/lights (transforms baked, media separated, light table built)
+ * and build the device BVH.  Host-only: no GPU needed.  lights may be -1. */
+int rt_scene_create(const rt_tree* t, int world, int lights, rt_scene** out);
+int rt_scene_destroy(rt_scene* s);
+
+typedef struct {
+  int32_t n_spheres, n_quads, n_triangles;
+  int32_t n_world_prims, n_media, n_lights;
+  int32_t n_bvh_nodes, bvh_depth, max_leaf;
+  int32_t n_materials, n_textures, n_images, n_perlins;
+  int32_t medium_draws; /* total free-flight draws per vertex */
+  int64_t device_bytes; /* scene bytes uploaded to HBM */
+} rt_scene_info;
+int rt_scene_info_get(const rt_scene* s, rt_scene_info* out);
+
+/* BVH export for structural tests: nodes as 16 floats
+ * {b0min[3], b0max[3], b1min[3], b1max[3], child0 bits, child1 bits, 0, 0},
+ * leaf child encoding documented in DESIGN.md.  Pass NULL to query counts. */
+int rt_scene_export_bvh(const rt_scene* s, float* nodes, int32_t* n_nodes, uint32_t* prim_refs,
+                        int32_t* n_refs, uint32_t* root);
+/* world-prim float AABBs in prim-ref order (6 floats each) */
+int rt_scene_export_prim_bounds(const rt_scene* s, float* bounds, int32_t* n);
+
+enum { RT_FLAG_PROFILE = 1 }; /* time every kernel with HIP events */
+
+typedef struct {
+  uint64_t seed;       /* render_seed */
+  int32_t device;      /* HIP device ordinal */
+  int32_t rank;        /* row-interleaved shard: rows r with r % nranks == rank */
+  int32_t nranks;
+  int32_t path_slots;  /* wavefront capacity; 0 = auto */
+  int32_t chunk;       /* samples per work chunk; 0 = auto */
+  int32_t flags;       /* RT_FLAG_* */
+  void* stream;        /* hipStream_t to enqueue on; NULL = library stream */
+  /* path trace of one sample (debugging): when trace_out != NULL the vertices
+   * of sample trace_sample of global pixel trace_pixel are written as 12 floats
+   * {o.xyz, time, d.xyz, vertex, t, u, v, prim-ref bits} per world.Hit call,
+   * up to trace_cap vertices; unused entries have vertex = -1. */
+  int64_t trace_pixel;
+  int32_t trace_sample;
+  int32_t trace_cap;
+  float* trace_out;
+} rt_render_opts;
+
+typedef struct {
+  uint64_t samples;      /* W*rows*spp_sqrt^2 rendered by this call */
+  uint64_t segments;     /* closest-hit queries (world.Hit calls, camera.go:300) */
+  uint64_t stack_pushes; /* clamp-vertex weights spilled to HBM */
+  uint64_t extend_rays;  /* total rays processed by extend launches */
+  uint64_t shade_rays;
+  double ms_total;       /* render wall time (host, incl. sync) */
+  double ms_extend;      /* summed extend-kernel time (RT_FLAG_PROFILE) */
+  double ms_shade;
+  double ms_other;
+  int32_t n_extend_launches;
+  int32_t n_shade_launches;
+  int32_t iterations;
+  int32_t rows;          /* rows rendered by this rank */
+} rt_stats;
+
+/* Render this rank's rows; out_rgb (host) receives linear mean RGB
+ * [rows][W][3] fp32, rows = rows r with r % nranks == rank in increasing order. */
+int rt_render(rt_scene* s, const rt_camera* cam, const rt_render_opts* opts, float* out_rgb,
+              rt_stats* stats);
+/* Same, but out_rgb is a device pointer on opts->device (e.g. a torch tensor);
+ * work is enqueued on opts->stream and the call returns after it completes. */
+int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_render_opts* opts,
+                     float* out_rgb_device, rt_stats* stats);
+
+/* Output: PrintColor vec/color.go:23-46 (NaN->0, sqrt gamma, clamp .99999, x256). */
+int rt_quantize(const float* rgb, int64_t n_pixels, uint8_t* out);
+/* PPM P3 text exactly as camera.go:160 + PrintColor; returns bytes written
+ * (call with out = NULL to size). */
+int64_t rt_format_ppm(const float* rgb, int w, int h, char* out, int64_t cap);
+
+/* Demo scenes mirroring main.go (by name or the main.go -S number).
+ * names: book1, book2, book3, simple_light, quads, cornell, cornell_smoke, model
+ * The camera receives the scene's settings; override fields afterwards. */
+int rt_demo_scene(rt_tree* t, const char* name, const char* asset_dir, rt_camera* cam,
+                  int* world, int* lights);
+int rt_demo_scene_name(int s_number, const char** name_out);
+
+/* Number of HIP devices visible (0 on a CPU-only host; never aborts). */
+int rt_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_ABI_H */

@@ -1,0 +1,98 @@
+/*
+ * rt_rng.h — the counter-based random stream shared by the HIP path tracer and
+ * the CPU oracle.  Part of the parity contract, not of the algorithm under test.
+ *
+ * The reference draws every random number from Go's process-global, unseeded
+ * math/rand (camera.go:268,278-279; pdf.go:70; objects.go:71-72,162,372-373;
+ * medium.go:47; materials.go:112; vec.go:28,178-179), so its renders are not
+ * reproducible.  Here every draw is a pure function of
+ *     (seed, global pixel index, sample index, path vertex, group, lane)
+ * computed with Philox4x32-10 (Salmon et al., SC'11; Random123 constants).
+ * Both implementations therefore consume identical uniforms no matter in which
+ * order, on which rank, or in which wavefront slot a path is processed.
+ *
+ * Uniforms are 24-bit: u = (x >> 8) * 2^-24 in [0, 1 - 2^-24], exactly
+ * representable in float and double, so the fp32 device path and the fp64
+ * oracle start every path from bit-identical random numbers.
+ *
+ * Dimension map (one Philox call = 4 lanes):
+ *   camera  group 0: [0] jitter x (inner stratum s_j)  [1] jitter y (outer s_i)
+ *                    [2] ray time                       [3] unused
+ *   camera  group 1: [0],[1] defocus disk (only when DefocusAngle > 0)
+ *   vertex k group 0: [0] coin (mixture pdf pdf.go:70 / dielectric materials.go:112)
+ *                     [1] light pick (hittable.go:102 rand.Intn) — 24-bit integer
+ *                     [2],[3] direction sample (cosine, light, sphere, fuzz)
+ *   vertex k group 1+g: medium free-flight draws 4g..4g+3 (medium.go:47)
+ */
+#ifndef RT_RNG_H
+#define RT_RNG_H
+
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define RT_RNG_FN __host__ __device__ __forceinline__
+#else
+#define RT_RNG_FN static inline
+#endif
+
+#define RT_PHILOX_M0 0xD2511F53u
+#define RT_PHILOX_M1 0xCD9E8D57u
+#define RT_PHILOX_W0 0x9E3779B9u
+#define RT_PHILOX_W1 0xBB67AE85u
+
+/* stream ids */
+#define RT_STREAM_CAMERA 0xFFFFFFF0u
+#define RT_STREAM(vertex, group) ((((uint32_t)(vertex)) << 4) | (uint32_t)(group))
+
+typedef struct {
+  uint32_t v[4];
+} rt_u32x4;
+
+RT_RNG_FN rt_u32x4 rt_philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                    uint32_t k0, uint32_t k1) {
+  for (int r = 0; r < 10; ++r) {
+    if (r) {
+      k0 += RT_PHILOX_W0;
+      k1 += RT_PHILOX_W1;
+    }
+    uint64_t p0 = (uint64_t)RT_PHILOX_M0 * (uint64_t)c0;
+    uint64_t p1 = (uint64_t)RT_PHILOX_M1 * (uint64_t)c2;
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    uint32_t n0 = hi1 ^ c1 ^ k0;
+    uint32_t n2 = hi0 ^ c3 ^ k1;
+    c0 = n0;
+    c1 = lo1;
+    c2 = n2;
+    c3 = lo0;
+  }
+  rt_u32x4 out;
+  out.v[0] = c0;
+  out.v[1] = c1;
+  out.v[2] = c2;
+  out.v[3] = c3;
+  return out;
+}
+
+/* Four raw 32-bit draws for (pixel, sample, stream). */
+RT_RNG_FN rt_u32x4 rt_rng_draw(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t stream) {
+  return rt_philox4x32_10(pixel, sample, stream, 0u, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+RT_RNG_FN uint32_t rt_u24(uint32_t x) { return x >> 8; }
+
+RT_RNG_FN float rt_unit_f(uint32_t x) { return (float)(x >> 8) * 5.9604644775390625e-08f; }
+
+RT_RNG_FN double rt_unit_d(uint32_t x) { return (double)(x >> 8) * 5.9604644775390625e-08; }
+
+/* rand.Intn(n) replacement: exact integer map of the 24-bit uniform to [0, n). */
+RT_RNG_FN uint32_t rt_pick(uint32_t x, uint32_t n) {
+  return (uint32_t)(((uint64_t)(x >> 8) * (uint64_t)n) >> 24);
+}
+
+/* residual 24-bit uniform left after rt_pick (used for nested light lists) */
+RT_RNG_FN uint32_t rt_pick_residual(uint32_t x, uint32_t n) {
+  return (uint32_t)((((uint64_t)(x >> 8) * (uint64_t)n) & 0xFFFFFFu) << 8);
+}
+
+#endif /* RT_RNG_H */

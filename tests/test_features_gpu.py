@@ -1,0 +1,28 @@
+"""Per-feature GPU-vs-oracle parity: one small scene per reference feature.
+
+Tolerance as in test_parity_gpu.py: >= 99 % of linear-RGB
+channels within 1e-3 * max(1, |ref|), 8-bit output equal for >= 99 %.
+"""
+import os
+
+import pytest
+
+from tests import scenes
+from tests.parity import compare
+
+pytestmark = pytest.mark.gpu
+ASSETS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets")
+
+
+@pytest.mark.parametrize("name", scenes.FEATURES)
+def test_feature_parity(rt, oracle, gpu, name):
+    t, cam, w, l = scenes.build(rt, name, ASSETS)
+    with rt.Scene(t, w, l) as sc:
+        img, st = sc.render(cam, seed=11)
+    ref, ost = oracle.render(t, w, l, cam, seed=11, threads=8)
+    m = compare(img, ref)
+    print(name, m, st["segments"], ost["segments"])
+    assert st["samples"] == ost["samples"]
+    assert abs(st["segments"] - ost["segments"]) <= 0.01 * ost["segments"] + 10
+    assert m["frac_close"] >= 0.99, m
+    assert m["q_equal"] >= 0.99, m
