@@ -276,9 +276,12 @@ class Scene:
         check(lib().rt_scene_export_prim_bounds(self._p, bounds.ctypes.data or None, C.byref(n)))
         return nodes, refs, int(root.value), bounds
 
+    MODES = {"auto": 0, "wavefront": 1, "fused": 2}
+
     @staticmethod
-    def _opts(seed, device, rank, nranks, path_slots, chunk, profile, stream):
+    def _opts(seed, device, rank, nranks, path_slots, chunk, profile, stream, mode="auto"):
         o = RtRenderOpts()
+        o.mode = Scene.MODES[mode]
         o.seed = seed
         o.device = device
         o.rank = rank
@@ -290,7 +293,7 @@ class Scene:
         return o
 
     def render(self, camera, seed=1, device=0, rank=0, nranks=1, path_slots=0, chunk=0,
-               profile=False, trace=None):
+               profile=False, trace=None, mode="auto"):
         """Render this rank's rows -> (float32 [rows, W, 3], stats dict).
 
         trace=(pixel, sample) additionally returns stats["trace"]: float32 [V, 12]
@@ -301,7 +304,7 @@ class Scene:
         out = np.zeros((rows, d.width, 3), np.float32)
         st = RtStats()
         c = camera.to_c()
-        o = self._opts(seed, device, rank, nranks, path_slots, chunk, profile, None)
+        o = self._opts(seed, device, rank, nranks, path_slots, chunk, profile, None, mode)
         tbuf = None
         if trace is not None:
             tbuf = np.zeros((d.max_depth + 1, 12), np.float32)
@@ -315,11 +318,11 @@ class Scene:
         return out, res
 
     def render_device(self, camera, out_ptr, seed=1, device=0, rank=0, nranks=1, path_slots=0,
-                      chunk=0, profile=False, stream=None):
+                      chunk=0, profile=False, stream=None, mode="auto"):
         """Render into a device buffer (e.g. torch tensor .data_ptr()) on `stream`."""
         st = RtStats()
         c = camera.to_c()
-        o = self._opts(seed, device, rank, nranks, path_slots, chunk, profile, stream)
+        o = self._opts(seed, device, rank, nranks, path_slots, chunk, profile, stream, mode)
         check(lib().rt_render_device(self._p, C.byref(c), C.byref(o), C.c_void_p(out_ptr),
                                      C.byref(st)))
         return {f: getattr(st, f) for f, _ in RtStats._fields_}

@@ -24,6 +24,7 @@ RT_NOISE_PERLIN, RT_NOISE_MARBLE, RT_NOISE_TURBULENT = 1, 2, 3
 (RT_NODE_LIST, RT_NODE_BVH, RT_NODE_SPHERE, RT_NODE_QUAD, RT_NODE_TRIANGLE,
  RT_NODE_TRANSLATE, RT_NODE_ROTATE_Y, RT_NODE_MEDIUM) = range(8)
 RT_FLAG_PROFILE = 1
+RT_MODE_AUTO, RT_MODE_WAVEFRONT, RT_MODE_FUSED = 0, 1, 2
 
 D3 = C.c_double * 3
 
@@ -63,7 +64,7 @@ class RtRenderOpts(C.Structure):
     _fields_ = [
         ("seed", C.c_uint64), ("device", C.c_int32), ("rank", C.c_int32),
         ("nranks", C.c_int32), ("path_slots", C.c_int32), ("chunk", C.c_int32),
-        ("flags", C.c_int32), ("stream", C.c_void_p),
+        ("flags", C.c_int32), ("mode", C.c_int32), ("stream", C.c_void_p),
         ("trace_pixel", C.c_int64), ("trace_sample", C.c_int32), ("trace_cap", C.c_int32),
         ("trace_out", C.c_void_p),
     ]
@@ -77,7 +78,8 @@ class RtStats(C.Structure):
         ("ms_extend", C.c_double), ("ms_shade", C.c_double),
         ("ms_other", C.c_double), ("n_extend_launches", C.c_int32),
         ("n_shade_launches", C.c_int32), ("iterations", C.c_int32),
-        ("rows", C.c_int32),
+        ("rows", C.c_int32), ("mode", C.c_int32), ("path_slots", C.c_int32),
+        ("ms_fused", C.c_double),
     ]
 
 

@@ -1,0 +1,697 @@
+// rt_path.h — per-path device logic shared by the wavefront and fused kernels:
+// launch parameters, camera rays, closest-hit traversal, media, textures,
+// light sampling and the shading core (one rayColor vertex, camera.go:293-331).
+// The shading core is templated on where path state lives: HBM structure-of-
+// arrays (wavefront kernels) or registers (fused persistent kernel).
+#pragma once
+#include "rt_kernels.h"
+
+namespace rt {
+
+constexpr int kLdsNodes = 512;   // BVH nodes staged in LDS per workgroup (32 KB)
+constexpr int kStack = 64;       // traversal stack entries per lane
+constexpr int kMaxIt = 1 << 16;  // per-iteration counter slots (no per-iteration memsets)
+constexpr int kXcd = 8;          // queue counters are sharded per XCD (blockIdx % 8)
+
+enum : uint32_t { F_PEND = 1u, F_PRE = 2u, F_NONFINITE = 4u };
+enum { OUT_DEAD = 0, OUT_ALIVE = 1, OUT_NEED_CHUNK = 2 };
+
+struct Counters {
+  unsigned long long segments;
+  unsigned long long pushes;
+  uint32_t chunk_head;
+  uint32_t _pad[13];
+  uint32_t cnt[kMaxIt][kXcd];  // per-XCD queue lengths entering iteration i
+};
+
+struct Params {
+  DevScene sc;
+  // camera (initialize camera.go:179-253, converted to fp32)
+  float p00r[3], du[3], dv[3], cc[3], dku[3], dkv[3];  // p00r = pixel00 - center
+  float bg[3];
+  float recip_s, maxc;
+  int s, defocus, max_depth;
+  int width, rank, nranks;
+  uint32_t npix;       // pixels of this rank
+  uint32_t K;          // samples per chunk
+  uint32_t n_chunks;
+  uint32_t P;          // path slots (stack column count)
+  uint32_t ss;         // s*s
+  uint64_t seed;
+  // wavefront state (SoA, slot-indexed)
+  F4* ray_o;   // origin | time
+  F4* ray_d;   // direction | 0
+  F4* hit;     // t, u, v, prim ref bits
+  uint2* path; // chunk, packed(j:12 | vertex:8 | nstack:8 | flags:4)
+  F4* pend;    // pending clamp-vertex weight (top of the weight stack)
+  F4* pre;     // camera-side product of specular attenuations
+  F4* acc;     // chunk accumulator
+  F4* stack;   // [vertex][slot] clamp-vertex weights spilled to HBM
+  uint32_t* queue[2];  // each kXcd segments of P entries
+  Counters* ctr;
+  unsigned long long* accum;  // 3 planes x npix, fixed point 2^-32
+  uint32_t* pflags;           // per pixel NaN (bits 0-2) / Inf (bits 3-5)
+  F4* trace;                  // debug path trace (3 F4 per vertex) or null
+  uint32_t trace_gpix, trace_sample;
+  int trace_cap;
+};
+
+RT_D uint32_t pack_path(uint32_t j, uint32_t k, uint32_t nst, uint32_t flags) {
+  return (j & 0xFFFu) | ((k & 0xFFu) << 12) | ((nst & 0xFFu) << 20) | ((flags & 0xFu) << 28);
+}
+
+RT_D uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+RT_D uint32_t prefix_count(unsigned long long m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+RT_D uint32_t wave_uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// chunk c -> (local pixel, global pixel, first sample).  Chunks are pixel-fastest
+// so a wave's consecutive chunks are adjacent pixels (coherent camera rays) and
+// concurrently flushed chunks touch different accumulators.
+struct Ids {
+  uint32_t lpix, gpix, row, col, sample0, count;
+};
+RT_D Ids chunk_ids(const Params& P, uint32_t chunk) {
+  Ids r;
+  r.lpix = chunk % P.npix;
+  uint32_t sub = chunk / P.npix;
+  uint32_t row_l = r.lpix / (uint32_t)P.width;
+  r.col = r.lpix - row_l * (uint32_t)P.width;
+  r.row = row_l * (uint32_t)P.nranks + (uint32_t)P.rank;
+  r.gpix = r.row * (uint32_t)P.width + r.col;
+  r.sample0 = sub * P.K;
+  r.count = min(P.K, P.ss - r.sample0);
+  return r;
+}
+
+// getRay camera.go:256-270 + sampleSquareStratified :277-282 + defocusDiskSample :285-290
+RT_D void camera_ray(const Params& P, const Ids& id, uint32_t sample, f3& o, f3& d, float& time) {
+  rt_u32x4 r = rt_rng_draw(P.seed, id.gpix, sample, RT_STREAM_CAMERA);
+  uint32_t si = sample / (uint32_t)P.s, sj = sample - si * (uint32_t)P.s;
+  float px = (((float)sj + rt_unit_f(r.v[0])) * P.recip_s) - 0.5f;
+  float py = (((float)si + rt_unit_f(r.v[1])) * P.recip_s) - 0.5f;
+  float fx = (float)id.col + px, fy = (float)id.row + py;
+  // pixelSample - rayOrigin rearranged as (pixel00 - center) + du*fx + dv*fy - disk:
+  // the same vector without fp32 cancellation against large camera coordinates
+  d = mk3(P.p00r[0] + P.du[0] * fx + P.dv[0] * fy, P.p00r[1] + P.du[1] * fx + P.dv[1] * fy,
+          P.p00r[2] + P.du[2] * fx + P.dv[2] * fy);
+  o = mk3(P.cc[0], P.cc[1], P.cc[2]);
+  if (P.defocus) {
+    rt_u32x4 q = rt_rng_draw(P.seed, id.gpix, sample, RT_STREAM_CAMERA | 1u);
+    f3 dk = uniform_disk(rt_unit_f(q.v[0]), rt_unit_f(q.v[1]));
+    f3 off = mk3(P.dku[0], P.dku[1], P.dku[2]) * dk.x + mk3(P.dkv[0], P.dkv[1], P.dkv[2]) * dk.y;
+    o = o + off;
+    d = d - off;
+  }
+  time = rt_unit_f(r.v[2]);
+}
+
+// ------------------------------------------------------------- traversal ---
+struct Hit {
+  float t, u, v;
+  uint32_t ref;
+};
+
+RT_D void slab(const F4& lo, const F4& hi, f3 o, f3 inv, float tmin, float tmax, bool& hit,
+               float& tnear) {
+  float tx0 = (lo.x - o.x) * inv.x, tx1 = (hi.x - o.x) * inv.x;
+  float ty0 = (lo.y - o.y) * inv.y, ty1 = (hi.y - o.y) * inv.y;
+  float tz0 = (lo.z - o.z) * inv.z, tz1 = (hi.z - o.z) * inv.z;
+  float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
+  float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+  hit = t0 <= t1 * 1.00000024f;  // 2 ulp slack: conservative for flat boxes
+  tnear = t0;
+}
+
+// Closest hit over the world BVH (replaces BVHNode.Hit bvh.go:69-82 +
+// HittableList.Hit hittable.go:122-138 + AABB.Hit aabb.go:90-113).
+RT_D void trace_world(const DevScene& sc, const F4* lnodes, int nl, f3 o, f3 d, float time,
+                      float tmin, Hit& best) {
+  if (sc.root == PRIM_NONE) return;
+  f3 inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  uint32_t stack[kStack];
+  int sp = 0;
+  uint32_t cur = sc.root;
+  for (;;) {
+    if (!(cur & LEAF_BIT)) {
+      F4 a0, a1, b0, b1;
+      if ((int)cur < nl) {
+        a0 = lnodes[4 * cur + 0];
+        a1 = lnodes[4 * cur + 1];
+        b0 = lnodes[4 * cur + 2];
+        b1 = lnodes[4 * cur + 3];
+      } else {
+        const F4* g = sc.nodes + 4 * (size_t)cur;
+        a0 = g[0];
+        a1 = g[1];
+        b0 = g[2];
+        b1 = g[3];
+      }
+      bool h0, h1;
+      float t0, t1;
+      slab(a0, a1, o, inv, tmin, best.t, h0, t0);
+      slab(b0, b1, o, inv, tmin, best.t, h1, t1);
+      uint32_t c0 = fbits(a0.w), c1 = fbits(a1.w);
+      if (h0 && h1) {
+        uint32_t nearc = t0 <= t1 ? c0 : c1, farc = t0 <= t1 ? c1 : c0;
+        if (sp < kStack) stack[sp++] = farc;
+        cur = nearc;
+        continue;
+      }
+      if (h0) {
+        cur = c0;
+        continue;
+      }
+      if (h1) {
+        cur = c1;
+        continue;
+      }
+    } else {
+      uint32_t first = (cur >> 4) & 0x7FFFFFFu, count = (cur & 15u) + 1u;
+      for (uint32_t k = 0; k < count; ++k) {
+        uint32_t ref = sc.refs[first + k];
+        float t, u, v;
+        if (hit_prim(sc, ref, o, d, time, tmin, best.t, t, u, v)) {
+          best.t = t;
+          best.u = u;
+          best.v = v;
+          best.ref = ref;
+        }
+      }
+    }
+    if (sp == 0) break;
+    cur = stack[--sp];
+  }
+}
+
+// closest boundary hit over (lo, hi) with each prim's own interval semantics
+RT_D bool boundary_hit(const DevScene& sc, const DevMedium& m, f3 o, f3 d, float time, double lo,
+                       double hi, double& t_out) {
+  bool any = false;
+  double best = hi;
+  for (uint32_t k = 0; k < m.bcount; ++k) {
+    double t;
+    if (hit_prim_d(sc, sc.medium_refs[m.bfirst + k], o, d, time, lo, best, t)) {
+      any = true;
+      best = t;
+    }
+  }
+  t_out = best;
+  return any;
+}
+
+// constantMedium.Hit medium.go:27-58, as a closest-hit candidate.  A medium
+// occurrence with multiplicity m keeps the smallest of m free-flight draws.
+// Interval arithmetic in fp64: the reference searches (t1 + 1e-4, inf) with
+// |t1| up to ~1e4 (book2 fog, R = 5000), below fp32 resolution.
+RT_D void trace_media(const Params& P, f3 o, f3 d, float time, float tmin, uint32_t gpix,
+                      uint32_t sample, uint32_t vertex, Hit& best) {
+  const DevScene& sc = P.sc;
+  rt_u32x4 r = {{0, 0, 0, 0}};
+  int cached_group = -1;
+  for (int mi = 0; mi < sc.n_media; ++mi) {
+    const DevMedium m = sc.media[mi];
+    double t1, t2;
+    if (!boundary_hit(sc, m, o, d, time, -(double)kInf, (double)kInf, t1)) continue;
+    if (!boundary_hit(sc, m, o, d, time, t1 + 0.0001, (double)kInf, t2)) continue;
+    t1 = fmax(t1, (double)tmin);
+    if (t1 >= t2) continue;
+    t1 = fmax(0.0, t1);
+    float ray_len = length(d);
+    double inside = (t2 - t1) * (double)ray_len;
+    float hd = kInf;
+    for (int k = 0; k < m.mult; ++k) {
+      int draw = m.draw_base + k;
+      int group = 1 + (draw >> 2);
+      if (group != cached_group) {
+        r = rt_rng_draw(P.seed, gpix, sample, RT_STREAM(vertex, group));
+        cached_group = group;
+      }
+      float u = rt_unit_f(r.v[draw & 3]);
+      hd = fminf(hd, m.neg_inv_density * logf(u));
+    }
+    if ((double)hd > inside) continue;
+    float tm = (float)(t1 + (double)(hd / ray_len));
+    if (tm < best.t) {
+      best.t = tm;
+      best.u = 0.0f;
+      best.v = 0.0f;
+      best.ref = prim_ref(PRIM_MEDIUM, (uint32_t)mi);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- shading --
+// Texture.Value texture.go:10-125 (checker chains resolved iteratively)
+RT_D float perlin_noise(const DevPerlin& pl, f3 p) {  // perlin.go:34-54
+  float fx = floorf(p.x), fy = floorf(p.y), fz = floorf(p.z);
+  float u = p.x - fx, v = p.y - fy, w = p.z - fz;
+  int i = (int)fx, j = (int)fy, k = (int)fz;
+  float uu = u * u * (3 - 2 * u), vv = v * v * (3 - 2 * v), ww = w * w * (3 - 2 * w);
+  float accum = 0.0f;
+  for (int di = 0; di < 2; ++di)
+    for (int dj = 0; dj < 2; ++dj)
+      for (int dk = 0; dk < 2; ++dk) {
+        int idx = pl.perm[0][(i + di) & 255] ^ pl.perm[1][(j + dj) & 255] ^ pl.perm[2][(k + dk) & 255];
+        F4 g = pl.ranvec[idx];
+        f3 wt = mk3(u - (float)di, v - (float)dj, w - (float)dk);
+        accum += ((float)di * uu + (float)(1 - di) * (1 - uu)) *
+                 ((float)dj * vv + (float)(1 - dj) * (1 - vv)) *
+                 ((float)dk * ww + (float)(1 - dk) * (1 - ww)) * dot(xyz(g), wt);
+      }
+  return accum;
+}
+RT_D float perlin_turb(const DevPerlin& pl, f3 p, int depth) {  // perlin.go:57-69
+  float accum = 0.0f, weight = 1.0f;
+  for (int i = 0; i < depth; ++i) {
+    accum += weight * perlin_noise(pl, p);
+    weight *= 0.5f;
+    p = p * 2.0f;
+  }
+  return fabsf(accum);
+}
+
+RT_D f3 tex_value(const DevScene& sc, int tex, float u, float v, f3 p) {
+  for (int guard = 0; guard < 64; ++guard) {
+    const DevTexture T = sc.texs[tex];
+    if (T.kind == RT_TEX_SOLID) return xyz(T.color);
+    if (T.kind == RT_TEX_CHECKER) {  // texture.go:50-60
+      float inv = T.color.w;
+      int x = (int)floorf(inv * p.x), y = (int)floorf(inv * p.y), z = (int)floorf(inv * p.z);
+      tex = ((x + y + z) % 2 == 0) ? T.a : T.b;
+      continue;
+    }
+    if (T.kind == RT_TEX_IMAGE) {  // texture.go:70-86 + PixelData imageLoader.go:52-62
+      const DevImage im = sc.images[T.a];
+      if (im.h <= 0) return mk3(0, 1, 1);
+      float uu = fabsf(fmodf(u, 1.0f));
+      float vv = 1.0f - fabsf(fmodf(v, 1.0f));
+      float fi = uu * (float)(im.w - 1), fj = vv * (float)(im.h - 1);
+      int i = isnan(fi) ? 0 : (int)fi, j = isnan(fj) ? 0 : (int)fj;
+      i = min(max(i, 0), im.w);
+      j = min(max(j, 0), im.h);
+      long idx = (long)j * im.w + i;
+      if (idx >= (long)im.w * im.h) return mk3(1.0f, 0.0f, 1.0f);  // magenta
+      const uint8_t* px = sc.texels + im.offset + 3 * idx;
+      const float s = 1.0f / 255.0f;
+      return mk3((float)px[0] * s, (float)px[1] * s, (float)px[2] * s);
+    }
+    // noise, texture.go:112-125
+    const DevPerlin& pl = sc.perlins[T.a];
+    float scale = T.color.w;
+    if (T.variant == RT_NOISE_MARBLE) {
+      float s = 0.5f * (1.0f + sinf(scale * p.z + 10.0f * perlin_turb(pl, p, 7)));
+      return mk3(s, s, s);
+    }
+    if (T.variant == RT_NOISE_TURBULENT) {
+      float s = perlin_turb(pl, p, 7);
+      return mk3(s, s, s);
+    }
+    float s = 0.5f * (1.0f + perlin_noise(pl, p * scale));
+    return mk3(s, s, s);
+  }
+  return mk3(0, 0, 0);
+}
+
+// Triangle.interpolateNormal objects.go:389-405
+RT_D f3 tri_normal(const DevScene& sc, uint32_t idx, float bu, float bv) {
+  const F4* at = sc.tri_attr + 6 * (size_t)idx;
+  uint32_t flags = fbits(sc.tri[3 * (size_t)idx + 2].w);
+  if (!(flags & TRI_HAS_NORMALS)) return xyz(at[0]);
+  float w = 1.0f - bu - bv;
+  f3 n = xyz(at[1]) * w + xyz(at[2]) * bu + xyz(at[3]) * bv;
+  return unit(n);
+}
+
+// light PdfValue: sphere objects.go:52-62, quad :152-160, triangle :356-367
+RT_D float prim_pdf(const DevScene& sc, uint32_t ref, f3 origin, f3 dir) {
+  uint32_t type = ref >> 30, idx = ref & 0x3FFFFFFFu;
+  if (type == PRIM_SPHERE) {
+    float t;
+    if (!hit_sphere(sc, idx, origin, dir, 0.0f, 0.0001f, kInf, t)) return 0.0f;
+    const F4 cr = sc.sph_cr[idx];
+    f3 oc = xyz(cr) - origin;
+    float dist2 = dot(oc, oc);
+    float cmax = sqrtf(1.0f - cr.w * cr.w / dist2);
+    return 1.0f / (2.0f * kPi * (1.0f - cmax));
+  }
+  float t, u, v, area;
+  f3 n;
+  if (type == PRIM_QUAD) {
+    if (!hit_quad(sc, idx, origin, dir, 0.001f, kInf, t, u, v)) return 0.0f;
+    const F4* q = sc.quad + 5 * (size_t)idx;
+    n = xyz(q[3]);
+    area = q[1].w;
+  } else {
+    if (!hit_tri(sc, idx, origin, dir, 0.001f, kInf, t, u, v)) return 0.0f;
+    n = tri_normal(sc, idx, u, v);
+    area = sc.tri[3 * (size_t)idx + 1].w;
+  }
+  float dist2 = t * t * dot(dir, dir);
+  float cosine = fabsf(dot(dir, n) / length(dir));
+  return dist2 / (cosine * area);
+}
+
+// HittableList.PdfValue hittable.go:89-97 over the flattened light table
+RT_D float lights_pdf(const DevScene& sc, f3 origin, f3 dir) {
+  float sum = 0.0f;
+  for (int i = 0; i < sc.n_lights; ++i) {
+    const DevLight L = sc.lights[i];
+    if (L.ref == PRIM_NONE) continue;
+    sum += L.weight * prim_pdf(sc, L.ref, origin, dir);
+  }
+  return sum;
+}
+
+// HittableList.Random hittable.go:98-103 + sphere/quad/Triangle.Random
+RT_D f3 lights_random(const DevScene& sc, f3 origin, const rt_u32x4& r) {
+  const float s0 = rt_unit_f(r.v[2]), s1 = rt_unit_f(r.v[3]);
+  int lo = 0, hi = sc.n_lights - 1;
+  if (sc.n_lights <= 0) return mk3(rt_unit_f(r.v[1]), s0, s1);  // vec.Random()
+  const uint32_t u24 = rt_u24(r.v[1]);
+  while (lo < hi) {  // last entry with lo24 <= u24
+    int mid = (lo + hi + 1) >> 1;
+    if (sc.lights[mid].lo24 <= u24) lo = mid;
+    else hi = mid - 1;
+  }
+  const uint32_t ref = sc.lights[lo].ref;
+  if (ref == PRIM_NONE) return mk3(rt_unit_f(r.v[1]), s0, s1);
+  uint32_t type = ref >> 30, idx = ref & 0x3FFFFFFFu;
+  if (type == PRIM_SPHERE) {  // sphere.Random + randomToSphere objects.go:63-80
+    const F4 cr = sc.sph_cr[idx];
+    f3 dir = xyz(cr) - origin;
+    float dist2 = dot(dir, dir);
+    Onb b = make_onb(dir);
+    float z = 1.0f + s1 * (sqrtf(1.0f - cr.w * cr.w / dist2) - 1.0f);
+    float phi = 2.0f * kPi * s0;
+    float tt = sqrtf(1.0f - z * z);
+    return onb_transform(b, mk3(cosf(phi) * tt, sinf(phi) * tt, z));
+  }
+  if (type == PRIM_QUAD) {  // quad.Random objects.go:161-165
+    const F4* q = sc.quad + 5 * (size_t)idx;
+    return (xyz(q[0]) + xyz(q[1]) * s0 + xyz(q[2]) * s1) - origin;
+  }
+  // Triangle.Random objects.go:369-385 (non-uniform barycentrics kept)
+  const F4* tr = sc.tri + 3 * (size_t)idx;
+  float r1 = s0, r2 = s1 * (1.0f - r1);
+  f3 v0 = xyz(tr[0]), v1 = v0 + xyz(tr[1]), v2 = v0 + xyz(tr[2]);
+  f3 p = v0 * (1.0f - r1 - r2) + v1 * r1 + v2 * r2;
+  return p - origin;
+}
+
+RT_D void flush_chunk(const Params& P, uint32_t chunk, f3 acc) {
+  const uint32_t lp = chunk % P.npix;
+  const float c[3] = {acc.x, acc.y, acc.z};
+  for (int ch = 0; ch < 3; ++ch) {
+    float v = c[ch];
+    if (isnan(v)) {
+      atomicOr(&P.pflags[lp], 1u << ch);
+    } else if (isinf(v)) {
+      atomicOr(&P.pflags[lp], 8u << ch);
+    } else {
+      float cl = fminf(fmaxf(v, -2147483648.0f), 2147483520.0f);
+      long long fx = (long long)(cl * 4294967296.0f);
+      atomicAdd(&P.accum[(size_t)ch * P.npix + lp], (unsigned long long)fx);
+    }
+  }
+}
+
+// ------------------------------------------------------------- path state --
+// One path.  In the fused kernel every field lives in registers; in the
+// wavefront kernels ray/key fields are loaded from SoA and pend/pre/acc are
+// touched in HBM only when a vertex needs them (SOA = true).
+struct Path {
+  f3 o, d;
+  float time;
+  uint32_t chunk, j, k, nst, flags;
+  f3 pend, pre, acc;
+  unsigned long long segs, pushes;  // per-lane statistics (fused kernel)
+};
+
+template <bool SOA>
+RT_D f3 get_pend(const Params& P, uint32_t slot, const Path& s) {
+  return SOA ? xyz(P.pend[slot]) : s.pend;
+}
+template <bool SOA>
+RT_D void set_pend(const Params& P, uint32_t slot, Path& s, f3 v) {
+  if (SOA) P.pend[slot] = {v.x, v.y, v.z, 0.0f};
+  else s.pend = v;
+}
+template <bool SOA>
+RT_D f3 get_pre(const Params& P, uint32_t slot, const Path& s) {
+  return SOA ? xyz(P.pre[slot]) : s.pre;
+}
+template <bool SOA>
+RT_D void set_pre(const Params& P, uint32_t slot, Path& s, f3 v) {
+  if (SOA) P.pre[slot] = {v.x, v.y, v.z, 0.0f};
+  else s.pre = v;
+}
+template <bool SOA>
+RT_D f3 get_acc(const Params& P, uint32_t slot, const Path& s) {
+  return SOA ? xyz(P.acc[slot]) : s.acc;
+}
+template <bool SOA>
+RT_D void set_acc(const Params& P, uint32_t slot, Path& s, f3 v) {
+  if (SOA) P.acc[slot] = {v.x, v.y, v.z, 0.0f};
+  else s.acc = v;
+}
+
+template <bool SOA>
+RT_D void store_ray(const Params& P, uint32_t slot, const Path& s) {
+  if (SOA) {
+    P.ray_o[slot] = {s.o.x, s.o.y, s.o.z, s.time};
+    P.ray_d[slot] = {s.d.x, s.d.y, s.d.z, 0.0f};
+    P.path[slot] = make_uint2(s.chunk, pack_path(s.j, s.k, s.nst, s.flags));
+  }
+}
+
+RT_D void load_path(const Params& P, uint32_t slot, Path& s) {
+  const F4 ro = P.ray_o[slot], rd = P.ray_d[slot];
+  const uint2 ps = P.path[slot];
+  s.o = xyz(ro);
+  s.time = ro.w;
+  s.d = xyz(rd);
+  s.chunk = ps.x;
+  s.j = ps.y & 0xFFFu;
+  s.k = (ps.y >> 12) & 0xFFu;
+  s.nst = (ps.y >> 20) & 0xFFu;
+  s.flags = ps.y >> 28;
+}
+
+// camera ray for sample j of `chunk` (path state reset)
+template <bool SOA>
+RT_D void start_sample(const Params& P, uint32_t slot, Path& s, uint32_t chunk, uint32_t j) {
+  Ids id = chunk_ids(P, chunk);
+  camera_ray(P, id, id.sample0 + j, s.o, s.d, s.time);
+  s.chunk = chunk;
+  s.j = j;
+  s.k = 0;
+  s.nst = 0;
+  s.flags = 0;
+  store_ray<SOA>(P, slot, s);
+}
+
+// One vertex of rayColor (camera.go:293-331) given its closest hit.
+// Returns OUT_ALIVE (continue with s.o/s.d), or OUT_NEED_CHUNK (chunk flushed).
+template <bool SOA>
+RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h) {
+  const DevScene& sc = P.sc;
+  const f3 o = s.o, d = s.d;
+  const float time = s.time;
+  const uint32_t ref = h.ref;
+  f3 lterm = mk3(0, 0, 0);
+  bool term = false;
+  if (ref == PRIM_NONE) {
+    lterm = mk3(P.bg[0], P.bg[1], P.bg[2]);  // camera.go:300-302
+    term = true;
+  } else {
+    const float t = h.t;
+    const f3 p = o + d * t;  // r.At(t)
+    const uint32_t type = ref >> 30, idx = ref & 0x3FFFFFFFu;
+    f3 nout;
+    float u = h.u, v = h.v;
+    int mat;
+    bool ff = true;
+    f3 n;
+    if (type == PRIM_SPHERE) {
+      const F4 cr = sc.sph_cr[idx], mv = sc.sph_mv[idx];
+      f3 cc = xyz(cr) + xyz(mv) * time;
+      nout = (p - cc) * (1.0f / cr.w);
+      mat = (int)fbits(mv.w);
+      ff = dot(d, nout) < 0;  // setFaceNormal hittable.go:27-34
+      n = ff ? nout : -nout;
+      if (sc.mats[mat]._pad != 0.0f) {  // texture reads u,v: calculateSphereUV objects.go:44-50
+        const F2 rs = sc.sph_uv[idx];
+        f3 no = mk3(rs.x * nout.x - rs.y * nout.z, nout.y, rs.y * nout.x + rs.x * nout.z);
+        float theta = acosf(-no.y);
+        float phi = atan2f(-no.z, no.x) + kPi;
+        u = phi / (2.0f * kPi);
+        v = theta / kPi;
+      }
+    } else if (type == PRIM_QUAD) {
+      const F4* q = sc.quad + 5 * (size_t)idx;
+      nout = xyz(q[3]);
+      mat = (int)fbits(q[2].w);
+      ff = dot(d, nout) < 0;
+      n = ff ? nout : -nout;
+    } else if (type == PRIM_TRI) {
+      nout = tri_normal(sc, idx, u, v);
+      mat = (int)fbits(sc.tri[3 * (size_t)idx].w);
+      ff = dot(d, nout) < 0;
+      n = ff ? nout : -nout;
+      uint32_t tf = fbits(sc.tri[3 * (size_t)idx + 2].w);
+      if (tf & TRI_HAS_UV) {  // objects.go:437-446
+        const F4* at = sc.tri_attr + 6 * (size_t)idx;
+        float w = 1.0f - u - v;
+        float tu = w * at[4].x + u * at[4].z + v * at[5].x;
+        float tv = w * at[4].y + u * at[4].w + v * at[5].y;
+        u = tu;
+        v = tv;
+      }
+    } else {  // medium hit medium.go:162-166: normal (1,0,0), front face
+      mat = sc.media[idx].phase_mat;
+      n = mk3(1, 0, 0);
+      ff = true;
+      u = v = 0.0f;
+    }
+    const DevMaterial M = sc.mats[mat];
+    if (M.kind == RT_MAT_DIFFUSE_LIGHT) {  // Emitted materials.go:150-155; Scatter false
+      lterm = ff ? tex_value(sc, M.tex, u, v, p) : mk3(0, 0, 0);
+      term = true;
+    } else {
+      const Ids id = chunk_ids(P, s.chunk);
+      const rt_u32x4 r = rt_rng_draw(P.seed, id.gpix, id.sample0 + s.j, RT_STREAM(s.k, 0));
+      f3 ndir;
+      bool clamp_vertex = false;
+      f3 weight;
+      if (M.kind == RT_MAT_METAL) {  // materials.go:70-79
+        f3 refl = unit(reflect(d, n));
+        ndir = refl + uniform_sphere(rt_unit_f(r.v[2]), rt_unit_f(r.v[3])) * M.param;
+        weight = xyz(M.albedo);
+      } else if (M.kind == RT_MAT_DIELECTRIC) {  // materials.go:94-130
+        float ior = M.param;
+        float ri = ff ? 1.0f / ior : ior;
+        f3 ud = unit(d);
+        float cs = fminf(dot(-ud, n), 1.0f);
+        float sn = sqrtf(1.0f - cs * cs);
+        bool cannot = ri * sn > 1.0f;
+        bool refl = cannot;
+        if (!cannot) {
+          float r0 = (1.0f - ior) / (1.0f + ior);
+          r0 = r0 * r0;
+          float refl_p = r0 + (1.0f - r0) * powf(1.0f - cs, 5.0f);
+          refl = refl_p > rt_unit_f(r.v[0]);
+        }
+        ndir = refl ? reflect(ud, n) : refract(ud, n, ri);
+        weight = mk3(1, 1, 1);
+      } else {  // lambertian materials.go:45-57 / isotropic :157-177 + mixture pdf.go:58-74
+        const bool iso = M.kind == RT_MAT_ISOTROPIC;
+        f3 att = tex_value(sc, M.tex, u, v, p);
+        Onb b;
+        if (!iso) b = make_onb(n);
+        if (rt_unit_f(r.v[0]) < 0.5f) {
+          ndir = lights_random(sc, p, r);
+        } else if (iso) {
+          ndir = uniform_sphere(rt_unit_f(r.v[2]), rt_unit_f(r.v[3]));
+        } else {
+          ndir = onb_transform(b, cosine_direction(rt_unit_f(r.v[2]), rt_unit_f(r.v[3])));
+        }
+        float bsdf_pdf, spdf;
+        if (iso) {
+          bsdf_pdf = 1.0f / (4.0f * kPi);
+          spdf = 1.0f / (4.0f * kPi);
+        } else {
+          f3 ud = unit(ndir);
+          bsdf_pdf = fmaxf(0.0f, dot(ud, b.w) / kPi);
+          float ct = dot(n, ud);
+          spdf = ct < 0.0f ? 0.0f : ct / kPi;
+        }
+        float pdf = 0.5f * lights_pdf(sc, p, ndir) + 0.5f * bsdf_pdf;
+        weight = (att * spdf) * (1.0f / pdf);
+        clamp_vertex = true;
+      }
+      // vertex bookkeeping (H1: the clamp is folded backwards at termination)
+      if (clamp_vertex) {
+        if (s.flags & F_PEND) {
+          f3 pv = get_pend<SOA>(P, slot, s);
+          P.stack[(size_t)s.nst * P.P + slot] = {pv.x, pv.y, pv.z, 0.0f};
+          ++s.nst;
+          ++s.pushes;
+        }
+        set_pend<SOA>(P, slot, s, weight);
+        s.flags |= F_PEND;
+      } else if (s.flags & F_PEND) {
+        set_pend<SOA>(P, slot, s, get_pend<SOA>(P, slot, s) * weight);
+      } else {
+        f3 w = (s.flags & F_PRE) ? get_pre<SOA>(P, slot, s) : mk3(1, 1, 1);
+        set_pre<SOA>(P, slot, s, w * weight);
+        s.flags |= F_PRE;
+      }
+      if (!finite3(weight)) s.flags |= F_NONFINITE;
+      ++s.k;
+      if ((int)s.k > P.max_depth) {  // rayColor(depth-1 < 0) == black, camera.go:294-296
+        term = true;
+        lterm = mk3(0, 0, 0);
+      } else {
+        s.o = p;
+        s.d = ndir;
+        store_ray<SOA>(P, slot, s);
+        return OUT_ALIVE;
+      }
+    }
+  }
+  // ---- termination: backward clamp fold (camera.go:316, :328-330)
+  f3 L = lterm;
+  const bool zero = lterm.x == 0.0f && lterm.y == 0.0f && lterm.z == 0.0f;
+  if (!(zero && !(s.flags & F_NONFINITE))) {
+    if (s.flags & F_PEND) L = clamp_contribution(get_pend<SOA>(P, slot, s) * L, P.maxc);
+    for (int kk = (int)s.nst - 1; kk >= 0; --kk)
+      L = clamp_contribution(xyz(P.stack[(size_t)kk * P.P + slot]) * L, P.maxc);
+    if (s.flags & F_PRE) L = get_pre<SOA>(P, slot, s) * L;
+  } else {
+    L = mk3(0, 0, 0);
+  }
+  f3 acc = L;
+  if (s.j > 0) acc = get_acc<SOA>(P, slot, s) + L;
+  const uint32_t count = chunk_ids(P, s.chunk).count;
+  if (s.j + 1 < count) {
+    set_acc<SOA>(P, slot, s, acc);
+    start_sample<SOA>(P, slot, s, s.chunk, s.j + 1);
+    return OUT_ALIVE;
+  }
+  flush_chunk(P, s.chunk, acc);
+  return OUT_NEED_CHUNK;
+}
+
+// Wave-batched work distribution: lanes that need a chunk take consecutive ids
+// from the wave's current batch; the batch is refilled with ONE returning
+// atomic per 64+ chunks (a single counter saturates near 88 returning atomics
+// per µs on MI355X, so per-event atomics would serialise the whole chip).
+struct WaveBatch {
+  uint32_t next, end;  // wave-uniform
+};
+RT_D uint32_t grab_chunk(const Params& P, WaveBatch& b, bool need) {
+  const unsigned long long m = __ballot(need);
+  if (!m) return 0xFFFFFFFFu;
+  const uint32_t n = (uint32_t)__popcll(m);
+  const uint32_t r = prefix_count(m);
+  const uint32_t avail = b.end - b.next;
+  uint32_t mine;
+  if (n <= avail) {
+    mine = b.next + r;
+    b.next += n;
+  } else {
+    const uint32_t grab = max(64u, n - avail);
+    uint32_t g = 0;
+    if (lane_id() == (uint32_t)(__ffsll((long long)m) - 1)) g = atomicAdd(&P.ctr->chunk_head, grab);
+    g = __shfl(g, __ffsll((long long)m) - 1);
+    mine = r < avail ? b.next + r : g + (r - avail);
+    b.next = g + (n - avail);
+    b.end = g + grab;
+  }
+  if (!need) return 0xFFFFFFFFu;
+  return mine < P.n_chunks ? mine : 0xFFFFFFFFu;
+}
+
+}  // namespace rt

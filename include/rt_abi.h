@@ -243,6 +243,12 @@ int rt_scene_export_prim_bounds(const rt_scene* s, float* bounds, int32_t* n);
 
 enum { RT_FLAG_PROFILE = 1 }; /* time every kernel with HIP events */
 
+/* execution strategy of the same per-vertex code (DESIGN.md "Kernels"):
+ *   WAVEFRONT: queue-driven extend / shade kernels, path state in HBM (SoA)
+ *   FUSED:     one persistent kernel, path state in registers
+ *   AUTO:      the faster one for the scene */
+enum { RT_MODE_AUTO = 0, RT_MODE_WAVEFRONT = 1, RT_MODE_FUSED = 2 };
+
 typedef struct {
   uint64_t seed;       /* render_seed */
   int32_t device;      /* HIP device ordinal */
@@ -251,6 +257,7 @@ typedef struct {
   int32_t path_slots;  /* wavefront capacity; 0 = auto */
   int32_t chunk;       /* samples per work chunk; 0 = auto */
   int32_t flags;       /* RT_FLAG_* */
+  int32_t mode;        /* RT_MODE_* */
   void* stream;        /* hipStream_t to enqueue on; NULL = library stream */
   /* path trace of one sample (debugging): when trace_out != NULL the vertices
    * of sample trace_sample of global pixel trace_pixel are written as 12 floats
@@ -276,6 +283,9 @@ typedef struct {
   int32_t n_shade_launches;
   int32_t iterations;
   int32_t rows;          /* rows rendered by this rank */
+  int32_t mode;          /* RT_MODE_* actually used */
+  int32_t path_slots;    /* concurrent paths (wavefront slots / fused lanes) */
+  double ms_fused;       /* fused-kernel time (RT_FLAG_PROFILE) */
 } rt_stats;
 
 /* Render this rank's rows; out_rgb (host) receives linear mean RGB

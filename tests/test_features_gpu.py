@@ -14,14 +14,15 @@ pytestmark = pytest.mark.gpu
 ASSETS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets")
 
 
+@pytest.mark.parametrize("mode", ["fused", "wavefront"])
 @pytest.mark.parametrize("name", scenes.FEATURES)
-def test_feature_parity(rt, oracle, gpu, name):
+def test_feature_parity(rt, oracle, gpu, name, mode):
     t, cam, w, l = scenes.build(rt, name, ASSETS)
     with rt.Scene(t, w, l) as sc:
-        img, st = sc.render(cam, seed=11)
+        img, st = sc.render(cam, seed=11, mode=mode)
     ref, ost = oracle.render(t, w, l, cam, seed=11, threads=8)
     m = compare(img, ref)
-    print(name, m, st["segments"], ost["segments"])
+    print(name, mode, m, st["segments"], ost["segments"])
     assert st["samples"] == ost["samples"]
     assert abs(st["segments"] - ost["segments"]) <= 0.01 * ost["segments"] + 10
     assert m["frac_close"] >= 0.99, m

@@ -27,18 +27,19 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("mode", ["fused", "wavefront"])
 @pytest.mark.parametrize("scene,width,spp,depth", CASES)
-def test_scene_parity(rt, oracle, gpu, scene, width, spp, depth):
+def test_scene_parity(rt, oracle, gpu, scene, width, spp, depth, mode):
     t, cam, w, l = rt.demo_scene(scene)
     cam.Width = width
     cam.SamplesPerPixel = spp
     if depth:
         cam.MaxDepth = depth
     with rt.Scene(t, w, l) as sc:
-        img, st = sc.render(cam, seed=7)
+        img, st = sc.render(cam, seed=7, mode=mode)
     ref, ost = oracle.render(t, w, l, cam, seed=7, threads=8)
     m = compare(img, ref)
-    print(scene, m, st["segments"], ost["segments"])
+    print(scene, mode, m, st["segments"], ost["segments"])
     assert st["samples"] == ost["samples"]
     assert abs(st["segments"] - ost["segments"]) <= 0.01 * ost["segments"] + 10
     assert m["frac_close"] >= 0.99, m

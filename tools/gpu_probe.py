@@ -11,10 +11,13 @@ cam.Width = width
 cam.SamplesPerPixel = spp
 if scene == "book1":
     cam.AspectRatio = 1.5
+modes = sys.argv[4].split(",") if len(sys.argv) > 4 else ["fused", "wavefront"]
 with rt.Scene(t, w, l) as sc:
-    img, st = sc.render(cam, seed=1, profile=True)  # warm (upload)
-    t0 = time.time()
-    img, st = sc.render(cam, seed=1, profile=True)
-    dt = time.time() - t0
-print(json.dumps({"scene": scene, "W": width, "spp": spp, "s": dt, "Msamples_s": st["samples"] / dt / 1e6,
-                  "seg_per_sample": st["segments"] / st["samples"], **st}))
+    for mode in modes:
+        img, st = sc.render(cam, seed=1, profile=True, mode=mode)  # warm (upload)
+        t0 = time.time()
+        img, st = sc.render(cam, seed=1, profile=True, mode=mode)
+        dt = time.time() - t0
+        print(json.dumps({"scene": scene, "mode": mode, "W": width, "spp": spp, "s": round(dt, 4),
+                          "Msamples_s": round(st["samples"] / dt / 1e6, 2),
+                          "seg_per_sample": round(st["segments"] / st["samples"], 4), **st}), flush=True)
