@@ -37,25 +37,27 @@ RT_D float bitsf(uint32_t u) { return __uint_as_float(u); }
 RT_D F4 ldg4(const F4* p) { return *p; }
 
 // ------------------------------------------------------------- sampling ----
+// cos/sin(2*pi*u) for u in [0,1): v_cos_f32 / v_sin_f32 take their argument in
+// revolutions, so the sampling angles need no range reduction.
+RT_D float cos2pi(float u) { return __builtin_amdgcn_cosf(u); }
+RT_D float sin2pi(float u) { return __builtin_amdgcn_sinf(u); }
+
 // Distribution-identical closed forms of the reference's rejection samplers.
 // RandomUnitVector vec.go:159-167 (uniform on the sphere)
 RT_D f3 uniform_sphere(float u0, float u1) {
   float z = 1.0f - 2.0f * u0;
   float r = sqrtf(fmaxf(0.0f, 1.0f - z * z));
-  float phi = 2.0f * kPi * u1;
-  return {r * cosf(phi), r * sinf(phi), z};
+  return {r * cos2pi(u1), r * sin2pi(u1), z};
 }
 // RandomUnitDisk vec.go:149-156 (uniform in the disk)
 RT_D f3 uniform_disk(float u0, float u1) {
   float r = sqrtf(u0);
-  float phi = 2.0f * kPi * u1;
-  return {r * cosf(phi), r * sinf(phi), 0.0f};
+  return {r * cos2pi(u1), r * sin2pi(u1), 0.0f};
 }
-// RandomCosineDirection vec.go:177-186 (same formula)
+// RandomCosineDirection vec.go:177-186: phi = 2*pi*r1
 RT_D f3 cosine_direction(float r1, float r2) {
-  float phi = 2.0f * kPi * r1;
   float s = sqrtf(r2);
-  return {cosf(phi) * s, sinf(phi) * s, sqrtf(1.0f - r2)};
+  return {cos2pi(r1) * s, sin2pi(r1) * s, sqrtf(1.0f - r2)};
 }
 
 // NewONB onb.go:13-25 — note the 0.9 test is on the un-normalised vector

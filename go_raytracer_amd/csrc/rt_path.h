@@ -9,7 +9,8 @@
 namespace rt {
 
 constexpr int kLdsNodes = 512;   // BVH nodes staged in LDS per workgroup (32 KB)
-constexpr int kStack = 64;       // traversal stack entries per lane
+constexpr int kStack = 64;       // traversal stack entries per lane (LDS short stack + HBM overflow)
+constexpr int kShortStack = 12;  // LDS entries per lane (column layout: [entry][thread])
 constexpr int kMaxIt = 1 << 16;  // per-iteration counter slots (no per-iteration memsets)
 constexpr int kXcd = 8;          // queue counters are sharded per XCD (blockIdx % 8)
 
@@ -51,6 +52,8 @@ struct Params {
   Counters* ctr;
   unsigned long long* accum;  // 3 planes x npix, fixed point 2^-32
   uint32_t* pflags;           // per pixel NaN (bits 0-2) / Inf (bits 3-5)
+  uint32_t* ostack;            // traversal-stack overflow [kStack - kShortStack][stack_cols]
+  uint32_t stack_cols;         // = launched threads of the traversal kernel
   F4* trace;                  // debug path trace (3 F4 per vertex) or null
   uint32_t trace_gpix, trace_sample;
   int trace_cap;
@@ -126,28 +129,35 @@ RT_D void slab(const F4& lo, const F4& hi, f3 o, f3 inv, float tmin, float tmax,
 
 // Closest hit over the world BVH (replaces BVHNode.Hit bvh.go:69-82 +
 // HittableList.Hit hittable.go:122-138 + AABB.Hit aabb.go:90-113).
-RT_D void trace_world(const DevScene& sc, const F4* lnodes, int nl, f3 o, f3 d, float time,
-                      float tmin, Hit& best) {
+// LDS = true: the whole node array is staged in LDS (ds_read_b128); false: nodes
+// come from HBM/L2 (global_load_dwordx4).  The two are separate instantiations:
+// mixing both sources in one loop makes hipcc merge them into flat loads.
+// The traversal stack lives in LDS (kShortStack entries per lane, one column
+// per thread: conflict-free ds_read/write_b32) and overflows to HBM.
+struct TravStack {
+  uint32_t* lds;     // &lds_stack[0][threadIdx.x], stride blockDim.x
+  uint32_t* ovf;     // &ostack[slot], stride cols
+  uint32_t cols;
+  RT_D void push(int sp, uint32_t v) const {
+    if (sp < kShortStack) lds[sp * 256] = v;
+    else ovf[(size_t)(sp - kShortStack) * cols] = v;
+  }
+  RT_D uint32_t pop(int sp) const {
+    return sp < kShortStack ? lds[sp * 256] : ovf[(size_t)(sp - kShortStack) * cols];
+  }
+};
+
+template <bool LDS>
+RT_D void trace_world(const DevScene& sc, const F4* lnodes, const TravStack& stack, f3 o, f3 d,
+                      float time, float tmin, Hit& best) {
   if (sc.root == PRIM_NONE) return;
   f3 inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-  uint32_t stack[kStack];
   int sp = 0;
   uint32_t cur = sc.root;
   for (;;) {
     if (!(cur & LEAF_BIT)) {
-      F4 a0, a1, b0, b1;
-      if ((int)cur < nl) {
-        a0 = lnodes[4 * cur + 0];
-        a1 = lnodes[4 * cur + 1];
-        b0 = lnodes[4 * cur + 2];
-        b1 = lnodes[4 * cur + 3];
-      } else {
-        const F4* g = sc.nodes + 4 * (size_t)cur;
-        a0 = g[0];
-        a1 = g[1];
-        b0 = g[2];
-        b1 = g[3];
-      }
+      const F4* g = LDS ? lnodes + 4 * cur : sc.nodes + 4 * (size_t)cur;
+      const F4 a0 = g[0], a1 = g[1], b0 = g[2], b1 = g[3];
       bool h0, h1;
       float t0, t1;
       slab(a0, a1, o, inv, tmin, best.t, h0, t0);
@@ -155,7 +165,7 @@ RT_D void trace_world(const DevScene& sc, const F4* lnodes, int nl, f3 o, f3 d, 
       uint32_t c0 = fbits(a0.w), c1 = fbits(a1.w);
       if (h0 && h1) {
         uint32_t nearc = t0 <= t1 ? c0 : c1, farc = t0 <= t1 ? c1 : c0;
-        if (sp < kStack) stack[sp++] = farc;
+        if (sp < kStack) stack.push(sp++, farc);
         cur = nearc;
         continue;
       }
@@ -181,7 +191,7 @@ RT_D void trace_world(const DevScene& sc, const F4* lnodes, int nl, f3 o, f3 d, 
       }
     }
     if (sp == 0) break;
-    cur = stack[--sp];
+    cur = stack.pop(--sp);
   }
 }
 
@@ -384,9 +394,8 @@ RT_D f3 lights_random(const DevScene& sc, f3 origin, const rt_u32x4& r) {
     float dist2 = dot(dir, dir);
     Onb b = make_onb(dir);
     float z = 1.0f + s1 * (sqrtf(1.0f - cr.w * cr.w / dist2) - 1.0f);
-    float phi = 2.0f * kPi * s0;
-    float tt = sqrtf(1.0f - z * z);
-    return onb_transform(b, mk3(cosf(phi) * tt, sinf(phi) * tt, z));
+    float tt = sqrtf(1.0f - z * z);  // phi = 2*pi*s0
+    return onb_transform(b, mk3(cos2pi(s0) * tt, sin2pi(s0) * tt, z));
   }
   if (type == PRIM_QUAD) {  // quad.Random objects.go:161-165
     const F4* q = sc.quad + 5 * (size_t)idx;
@@ -426,7 +435,7 @@ struct Path {
   float time;
   uint32_t chunk, j, k, nst, flags;
   f3 pend, pre, acc;
-  unsigned long long segs, pushes;  // per-lane statistics (fused kernel)
+  uint32_t segs, pushes;  // per-lane statistics (fused kernel)
 };
 
 template <bool SOA>

@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stddef.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -29,8 +30,9 @@
 
 namespace rt {
 
-RT_D void stage_nodes(const Params& P, F4* lnodes, int& nl) {
-  nl = min(P.sc.n_nodes, kLdsNodes);
+// the whole BVH node array -> LDS (only used when n_nodes <= kLdsNodes)
+RT_D void stage_nodes(const Params& P, F4* lnodes) {
+  const int nl = min(P.sc.n_nodes, kLdsNodes);
   for (int i = threadIdx.x; i < 4 * nl; i += blockDim.x) lnodes[i] = P.sc.nodes[i];
   __syncthreads();
 }
@@ -45,9 +47,10 @@ RT_D void record_trace(const Params& P, const Path& s, const Hit& best) {
 }
 
 // closest hit of one path (world BVH + media), camera.go:300
-RT_D Hit intersect(const Params& P, const F4* lnodes, int nl, const Path& s) {
+template <bool LDS>
+RT_D Hit intersect(const Params& P, const F4* lnodes, const TravStack& ts, const Path& s) {
   Hit best = {kInf, 0.0f, 0.0f, PRIM_NONE};
-  trace_world(P.sc, lnodes, nl, s.o, s.d, s.time, 0.001f, best);
+  trace_world<LDS>(P.sc, lnodes, ts, s.o, s.d, s.time, 0.001f, best);
   if (P.sc.n_media > 0) {
     const Ids id = chunk_ids(P, s.chunk);
     trace_media(P, s.o, s.d, s.time, 0.001f, id.gpix, id.sample0 + s.j, s.k, best);
@@ -68,10 +71,13 @@ RT_D uint32_t queue_slot(const Params& P, const uint32_t* q, const uint32_t* cnt
   return q[(size_t)x * P.P + i];
 }
 
+template <bool LDS>
 __global__ __launch_bounds__(256) void k_extend(Params P, int it) {
-  __shared__ F4 lnodes[4 * kLdsNodes];
-  int nl;
-  stage_nodes(P, lnodes, nl);
+  __shared__ F4 lnodes[LDS ? 4 * kLdsNodes : 4];
+  __shared__ uint32_t lstack[kShortStack * 256];
+  if (LDS) stage_nodes(P, lnodes);
+  const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
+  const TravStack ts = {&lstack[threadIdx.x], P.ostack + gtid, P.stack_cols};
   const uint32_t sel = (uint32_t)it & 1u;
   uint32_t cnt[kXcd];
   uint32_t n = 0;
@@ -85,7 +91,7 @@ __global__ __launch_bounds__(256) void k_extend(Params P, int it) {
     const uint32_t slot = queue_slot(P, q, cnt, i);
     Path s;
     load_path(P, slot, s);
-    const Hit best = intersect(P, lnodes, nl, s);
+    const Hit best = intersect<LDS>(P, lnodes, ts, s);
     P.hit[slot] = {best.t, best.u, best.v, bitsf(best.ref)};
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&P.ctr->segments, (unsigned long long)n);
@@ -156,11 +162,13 @@ __global__ __launch_bounds__(256) void k_init(Params P) {
 }
 
 // ----------------------------------------------------------------- fused ---
-__global__ __launch_bounds__(256) void k_fused(Params P) {
-  __shared__ F4 lnodes[4 * kLdsNodes];
-  int nl;
-  stage_nodes(P, lnodes, nl);
+template <bool LDS, int WAVES>
+__global__ __launch_bounds__(256, WAVES) void k_fused(Params P) {
+  __shared__ F4 lnodes[LDS ? 4 * kLdsNodes : 4];
+  __shared__ uint32_t lstack[kShortStack * 256];
+  if (LDS) stage_nodes(P, lnodes);
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;  // weight-stack column
+  const TravStack ts = {&lstack[threadIdx.x], P.ostack + slot, P.stack_cols};
   Path s;
   s.segs = 0;
   s.pushes = 0;
@@ -174,19 +182,19 @@ __global__ __launch_bounds__(256) void k_fused(Params P) {
     }
     if (!__any(has)) break;
     if (has) {
-      const Hit best = intersect(P, lnodes, nl, s);
+      const Hit best = intersect<LDS>(P, lnodes, ts, s);
       ++s.segs;
       if (shade_core<false>(P, slot, s, best) == OUT_NEED_CHUNK) has = false;
     }
   }
-  unsigned long long segs = s.segs, pushes = s.pushes;
+  uint32_t segs = s.segs, pushes = s.pushes;
   for (int off = 32; off > 0; off >>= 1) {
     segs += __shfl_xor(segs, off);
     pushes += __shfl_xor(pushes, off);
   }
   if (lane_id() == 0) {
-    atomicAdd(&P.ctr->segments, segs);
-    atomicAdd(&P.ctr->pushes, pushes);
+    atomicAdd(&P.ctr->segments, (unsigned long long)segs);
+    atomicAdd(&P.ctr->pushes, (unsigned long long)pushes);
   }
 }
 
@@ -240,6 +248,8 @@ struct RenderState {
   Counters* ctr = nullptr;
   unsigned long long* accum = nullptr;
   uint32_t* pflags = nullptr;
+  uint32_t* ostack = nullptr;
+  uint32_t ostack_cols = 0;
   float* out = nullptr;
   uint32_t out_cap = 0;
   std::vector<hipEvent_t> events;
@@ -375,6 +385,23 @@ static int occupancy_blocks(const void* kernel, int device, int* out) {
   return RT_OK;
 }
 
+// fused-kernel register budget (waves per SIMD); RT_FUSED_WAVES overrides (A/B tests)
+static int fused_waves() {
+  const char* e = getenv("RT_FUSED_WAVES");
+  int w = e ? atoi(e) : 3;
+  return (w == 3 || w == 4) ? w : 2;
+}
+static const void* pick_fused(bool lds, int waves) {
+  if (lds) {
+    if (waves == 4) return (const void*)k_fused<true, 4>;
+    if (waves == 3) return (const void*)k_fused<true, 3>;
+    return (const void*)k_fused<true, 2>;
+  }
+  if (waves == 4) return (const void*)k_fused<false, 4>;
+  if (waves == 3) return (const void*)k_fused<false, 3>;
+  return (const void*)k_fused<false, 2>;
+}
+
 static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_opts* opts,
                        float* out_host, float* out_dev, rt_stats* stats) {
   if (!scene || !cam) return set_error(RT_ERR_INVALID, "rt_render: null scene/camera");
@@ -411,8 +438,10 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   const int depth_cap = cd.max_depth + 1;
   uint32_t P;
   int fused_blocks = 0;
+  const bool lds_nodes = s->h.nodes.size() / 4 <= (size_t)kLdsNodes;
+  const void* fused_kernel = pick_fused(lds_nodes, fused_waves());
   if (mode == RT_MODE_FUSED) {
-    if ((rc = occupancy_blocks((const void*)k_fused, o.device, &fused_blocks))) return rc;
+    if ((rc = occupancy_blocks(fused_kernel, o.device, &fused_blocks))) return rc;
     if (o.path_slots > 0) fused_blocks = std::max(1, std::min(fused_blocks, (o.path_slots + 255) / 256));
     P = (uint32_t)fused_blocks * 256u;
   } else {
@@ -424,9 +453,24 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
                          mode == RT_MODE_WAVEFRONT)))
     return rc;
   RenderState* st = s->state;
+  const void* extend_kernel =
+      lds_nodes ? (const void*)k_extend<true> : (const void*)k_extend<false>;
   if (mode == RT_MODE_WAVEFRONT && st->resident_blocks == 0 &&
-      (rc = occupancy_blocks((const void*)k_extend, o.device, &st->resident_blocks)))
+      (rc = occupancy_blocks(extend_kernel, o.device, &st->resident_blocks)))
     return rc;
+  // traversal-stack overflow columns: one per launched traversal thread
+  {
+    const uint32_t cols = mode == RT_MODE_FUSED ? P : (uint32_t)st->resident_blocks * 256u;
+    if (st->ostack_cols < cols) {
+      if (st->ostack) {
+        HIP_OK(hipFree(st->ostack));
+        st->allocs.erase(std::find(st->allocs.begin(), st->allocs.end(), (void*)st->ostack));
+        st->ostack = nullptr;
+      }
+      if ((rc = dalloc(st, &st->ostack, (size_t)(kStack - kShortStack) * cols))) return rc;
+      st->ostack_cols = cols;
+    }
+  }
 
   hipStream_t stream = (hipStream_t)o.stream;
   if (!stream) {
@@ -472,6 +516,8 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   p.ctr = st->ctr;
   p.accum = st->accum;
   p.pflags = st->pflags;
+  p.ostack = st->ostack;
+  p.stack_cols = st->ostack_cols;
 
   F4* dtrace = nullptr;
   if (o.trace_out && o.trace_cap > 0) {
@@ -510,7 +556,8 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
       if ((rc = next_event(&e0)) || (rc = next_event(&e1))) return rc;
       HIP_OK(hipEventRecord(e0, stream));
     }
-    hipLaunchKernelGGL(k_fused, dim3(fused_blocks), dim3(256), 0, stream, p);
+    void* args[] = {&p};
+    HIP_OK(hipLaunchKernel(fused_kernel, dim3(fused_blocks), dim3(256), args, 0, stream));
     HIP_OK(hipGetLastError());
     if (prof) {
       HIP_OK(hipEventRecord(e1, stream));
@@ -533,7 +580,9 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
           if ((rc = next_event(&e0)) || (rc = next_event(&e1)) || (rc = next_event(&e2))) return rc;
           HIP_OK(hipEventRecord(e0, stream));
         }
-        hipLaunchKernelGGL(k_extend, dim3(ext_blocks), dim3(256), 0, stream, p, iterations);
+        int it_arg = iterations;
+        void* eargs[] = {&p, &it_arg};
+        HIP_OK(hipLaunchKernel(extend_kernel, dim3(ext_blocks), dim3(256), eargs, 0, stream));
         if (prof) HIP_OK(hipEventRecord(e1, stream));
         hipLaunchKernelGGL(k_shade, dim3((n_est + 255) / 256), dim3(256), 0, stream, p,
                            iterations);

@@ -24,6 +24,7 @@ CASES = [
     ("book2", 48, 9, 0),
     ("cornell_smoke", 48, 9, 0),
     ("model:64x16", 64, 9, 0),
+    ("model:384x96", 40, 4, 0),  # 74K triangles: deep BVH, exercises the HBM stack overflow
 ]
 
 
