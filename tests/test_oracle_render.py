@@ -1,0 +1,55 @@
+"""Oracle self-consistency (CPU): determinism, rank interleaving, and the fp32
+twin against the fp64 restatement (statistical)."""
+import numpy as np
+import pytest
+
+from tests import scenes
+
+
+def small(rt, name, width=24, spp=9):
+    t, cam, w, l = rt.demo_scene(name)
+    cam.Width = width
+    cam.SamplesPerPixel = spp
+    return t, cam, w, l
+
+
+def test_deterministic(rt, oracle):
+    t, cam, w, l = small(rt, "cornell")
+    a, _ = oracle.render(t, w, l, cam, seed=5, threads=4)
+    b, _ = oracle.render(t, w, l, cam, seed=5, threads=2)
+    assert np.array_equal(a, b)
+    c, _ = oracle.render(t, w, l, cam, seed=6, threads=4)
+    assert not np.array_equal(a, c)
+
+
+def test_rank_interleave_is_bitwise(rt, oracle):
+    t, cam, w, l = small(rt, "book1")
+    full, _ = oracle.render(t, w, l, cam, seed=2, threads=4)
+    for n in (2, 3):
+        for r in range(n):
+            part, _ = oracle.render(t, w, l, cam, seed=2, threads=4, rank=r, nranks=n)
+            assert np.array_equal(part, full[r::n])
+
+
+# The naive fp32 twin (reference algorithm, every op in fp32) drifts at Cornell's
+# ~555-unit coordinates (+6.7 % segments, -3 % mean: flat boxes and self-hits);
+# the HIP path's robustness measures keep it within 0.01 % of fp64 there
+# (tests/test_parity_gpu.py).  The twin is checked on small-coordinate scenes.
+@pytest.mark.parametrize("name", ["quads", "simple_light"])
+def test_fp32_twin_statistics(rt, oracle, name):
+    t, cam, w, l = small(rt, name, width=32, spp=16)
+    a, sa = oracle.render(t, w, l, cam, seed=3, threads=8, precision=64)
+    b, sb = oracle.render(t, w, l, cam, seed=3, threads=8, precision=32)
+    assert abs(sa["segments"] - sb["segments"]) <= 0.01 * sa["segments"]
+    ma, mb = np.nanmean(a), np.nanmean(b)
+    assert abs(ma - mb) <= 0.01 * max(ma, 1e-3)
+
+
+def test_maxcontribution_clamp(rt, oracle):
+    """Every clamp vertex output has r+g+b <= MaxContribution (camera.go:334-341):
+    with a black background the pixel mean of a diffuse-first scene stays below M."""
+    t, cam, w, l = small(rt, "cornell", width=16, spp=4)
+    img, _ = oracle.render(t, w, l, cam, seed=1, threads=4)
+    # first-vertex light hits are unclamped emission (15,15,15); everything else <= 1.5
+    s = img.sum(axis=2)
+    assert (s[(s > 0) & (s < 40)] <= 1.5 + 1e-5).mean() > 0.5

@@ -1,0 +1,136 @@
+"""Host-side scene pipeline: flattening (transforms baked, media multiplicity,
+light table), the device BVH's structural invariants, and error behaviour.
+CPU-only: no device memory is touched."""
+import numpy as np
+import pytest
+
+from tests import scenes
+
+
+def info(rt, name):
+    t, cam, w, l = rt.demo_scene(name)
+    with rt.Scene(t, w, l) as sc:
+        return sc.info()
+
+
+def test_cornell_flattening(rt):
+    i = info(rt, "cornell")
+    # 5 walls + light + 2 boxes x 6 quads in the world, + the light copy for sampling
+    assert i["n_world_prims"] == 18 and i["n_quads"] == 19 and i["n_lights"] == 1
+    assert i["n_media"] == 0
+
+
+def test_book2_flattening(rt):
+    i = info(rt, "book2")
+    assert i["n_world_prims"] == 2400 + 1 + 1006  # boxes, light, spheres (1000 rotated)
+    assert i["n_media"] == 2 and i["medium_draws"] == 2  # flat world list: no duplication
+    assert i["n_images"] == 1 and i["n_perlins"] == 1
+
+
+def test_book1_scene_content(rt):
+    i = info(rt, "book1")
+    # ground + 3 big + sun + random small spheres (perlin orbs are never added, main.go:52-60)
+    assert 300 < i["n_world_prims"] < 484 + 5
+    assert i["n_lights"] == 1
+
+
+def test_medium_multiplicity_from_span1_leaf(rt):
+    """bvh.go:44-46 duplicates span-1 leaves: a medium there is tested twice."""
+    t, cam, w, l = scenes.dup_medium(rt)
+    with rt.Scene(t, w, l) as sc:
+        i = sc.info()
+    assert i["n_media"] == 1 and i["medium_draws"] == 2
+
+
+def test_scene_is_pure_function_of_seed(rt):
+    def fingerprint(seed):
+        t, cam, w, l = rt.demo_scene("book1", seed=seed)
+        with rt.Scene(t, w, l) as sc:
+            nodes, refs, root, bounds = sc.export_bvh()
+        return bounds.tobytes()
+    assert fingerprint(1) == fingerprint(1)
+    assert fingerprint(1) != fingerprint(2)
+
+
+@pytest.mark.parametrize("name", ["cornell", "book1", "book2", "quads", "model:96x24"])
+def test_bvh_invariants(rt, name):
+    t, cam, w, l = rt.demo_scene(name)
+    with rt.Scene(t, w, l) as sc:
+        nodes, refs, root, bounds = sc.export_bvh()
+        i = sc.info()
+    n = len(refs)
+    assert n == i["n_world_prims"]
+    seen = np.zeros(n, np.int32)
+
+    def leaf(code):
+        return (code >> 4) & 0x7FFFFFF, (code & 15) + 1
+
+    def check(code, lo, hi):
+        if code & 0x80000000:
+            first, cnt = leaf(code)
+            seen[first:first + cnt] += 1
+            b = bounds[first:first + cnt]
+            assert (b[:, :3] >= lo - 1e-6).all() and (b[:, 3:] <= hi + 1e-6).all()
+            return
+        nd = nodes[code]
+        c0 = int(nd[3:4].view(np.uint32)[0])
+        c1 = int(nd[7:8].view(np.uint32)[0])
+        for c, (blo, bhi) in ((c0, (nd[0:3], nd[4:7])), (c1, (nd[8:11], nd[12:15]))):
+            assert (blo >= lo - 1e-6).all() and (bhi <= hi + 1e-6).all()
+            check(c, blo, bhi)
+
+    big = np.full(3, np.inf, np.float32)
+    check(root, -big, big)
+    assert (seen == 1).all(), "every world prim is referenced by exactly one leaf"
+    assert i["max_leaf"] <= 16
+
+
+def test_light_table_matches_nested_picks(rt):
+    """lights = list(list(a, b), c): the flattened pick intervals must select
+    exactly what nested rand.Intn picks select (hittable.go:98-103)."""
+    import ctypes as C
+    t, cam, w, l = scenes.nested_lights(rt)
+    with rt.Scene(t, w, l) as sc:
+        assert sc.info()["n_lights"] == 3
+    # reproduce the table from the interval rule and compare with nested picks
+    for u24 in list(range(0, 1 << 24, 99991)) + [(1 << 24) - 1, (1 << 23), (1 << 24) // 3]:
+        top = (u24 * 2) >> 24
+        if top == 0:
+            r = (u24 * 2) & 0xFFFFFF
+            expect = (r * 2) >> 24  # a or b
+        else:
+            expect = 2  # c
+        lo = [0, -(-(1 << 24) // 4), -(-(1 << 24) // 2)]  # ceil(i/4), ceil(2/4) boundaries
+        got = max(i for i in range(3) if lo[i] <= u24)
+        assert got == expect
+
+
+def test_lights_must_have_pdf(rt):
+    t = rt.Tree()
+    m = t.lambertian((1, 1, 1))
+    s = t.sphere((0, 0, 0), 1, m)
+    world = t.list(s)
+    for bad in (t.translate(s, (1, 0, 0)), t.bvh(t.list(s)), t.rotate_y(s, 10)):
+        with pytest.raises(rt.RtError) as e:
+            rt.Scene(t, world, bad)
+        assert e.value.code == -2  # defaultPdfImpl log.Fatal in the reference
+
+
+def test_rotated_transforms_baked(rt):
+    """Translate(RotateY(box)) quads end up where rotateY/translate map them."""
+    t = rt.Tree()
+    m = t.lambertian((1, 1, 1))
+    b = t.translate(t.rotate_y(t.box((0, 0, 0), (1, 2, 3), m), 90), (10, 0, 0))
+    with rt.Scene(t, b, -1) as sc:
+        nodes, refs, root, bounds = sc.export_bvh()
+    lo, hi = bounds[:, :3].min(0), bounds[:, 3:].max(0)
+    # Ry(90): x' = z, z' = -x  -> box spans x in [0,3]+10, z in [-1,0]
+    assert np.allclose(lo, [10, 0, -1], atol=1e-4) and np.allclose(hi, [13, 2, 0], atol=1e-4)
+
+
+def test_demo_scene_numbers(rt):
+    import ctypes as C
+    name = C.c_char_p()
+    assert rt.lib().rt_demo_scene_name(6, C.byref(name)) == 0 and name.value == b"cornell"
+    assert rt.lib().rt_demo_scene_name(8, C.byref(name)) == 0 and name.value == b"model"
+    assert rt.lib().rt_demo_scene_name(9, C.byref(name)) < 0
