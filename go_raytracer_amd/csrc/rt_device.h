@@ -42,6 +42,14 @@ inline constexpr uint32_t leaf_code(uint32_t first, uint32_t count) {
 //   attr 6 x F4 = face normal, vn0, vn1, vn2, (uv0,uv1), (uv2,0,0)
 enum : uint32_t { TRI_HAS_NORMALS = 1u, TRI_HAS_UV = 2u };
 
+// ---- leaf records: the traversal's copy of each leaf entry (64 B, refs order)
+// Built at upload from the per-type arrays; the shading code keeps using those.
+//  sphere: Cd = c0.xyz | ref  ;  motion.xyz | r       ; 0 ; 0
+//  quad:   Q.xyz | ref        ;  n.xyz | D            ; A = v x w | 0 ; B = w x u | 0
+//          (alpha = w.(p x v) = p.A, beta = w.(u x p) = p.B: the triple products of
+//           quad.Hit objects.go:186-187 with the cross products hoisted)
+//  tri:    v0.xyz | ref       ;  e0.xyz | 0           ; e1.xyz | 0 ; 0
+
 struct DevMedium {           // constantMedium medium.go:13-18
   uint32_t bfirst, bcount;   // boundary prim refs in medium_refs
   float neg_inv_density;     // -1/rho
@@ -89,6 +97,7 @@ struct DevScene {
   const F4* tri_attr;
   const F4* nodes;
   const uint32_t* refs;
+  const F4* leafprims;  // 4 x F4 per leaf entry, parallel to refs (see "leaf records")
   uint32_t root;
   int32_t n_nodes;
   const DevMedium* media;
@@ -97,7 +106,7 @@ struct DevScene {
   int32_t medium_draws;
   const DevLight* lights;
   int32_t n_lights;
-  int32_t _pad0;
+  int32_t n_refs;       // leaf entries (records)
   const DevMaterial* mats;
   const DevTexture* texs;
   const uint8_t* texels;

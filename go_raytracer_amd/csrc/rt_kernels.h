@@ -29,7 +29,9 @@ RT_D f3 cross(f3 a, f3 b) {
   return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
 }
 RT_D float length(f3 a) { return sqrtf(dot(a, a)); }
-RT_D f3 unit(f3 a) { return a * (1.0f / length(a)); }  // UnitVector vec.go:125
+// v_rcp_f32 (1 ulp): no range-scaling fix-up sequence around the reciprocal
+RT_D float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+RT_D f3 unit(f3 a) { return a * rcp(length(a)); }  // UnitVector vec.go:125
 RT_D bool finite3(f3 a) { return isfinite(a.x) && isfinite(a.y) && isfinite(a.z); }
 
 RT_D uint32_t fbits(float f) { return __float_as_uint(f); }
@@ -179,6 +181,80 @@ RT_D bool hit_prim(const DevScene& sc, uint32_t ref, f3 o, f3 d, float time, flo
   }
   if (type == PRIM_QUAD) return hit_quad(sc, idx, o, d, tmin, tmax, t, u, v);
   return hit_tri(sc, idx, o, d, tmin, tmax, t, u, v);
+}
+
+// ---- leaf-record tests (traversal; same semantics as the per-type tests) ----
+RT_D bool hit_sphere_rec(const F4 r[4], f3 o, f3 d, float time, float tmin, float tmax,
+                         float& t_out) {
+  const F4 c0 = r[0], mv = r[1];
+  double cx = (double)c0.x + (double)time * (double)mv.x;
+  double cy = (double)c0.y + (double)time * (double)mv.y;
+  double cz = (double)c0.z + (double)time * (double)mv.z;
+  double ox = cx - (double)o.x, oy = cy - (double)o.y, oz = cz - (double)o.z;
+  double dx = d.x, dy = d.y, dz = d.z;
+  double a = dx * dx + dy * dy + dz * dz;
+  double h = dx * ox + dy * oy + dz * oz;
+  double rr = mv.w;
+  double c = ox * ox + oy * oy + oz * oz - rr * rr;
+  double disc = h * h - a * c;
+  if (disc < 0) return false;
+  double sq = sqrt(disc);
+  // (tmin < (h -/+ sq)/a < tmax) tested as tmin*a < q < tmax*a (a > 0): one division
+  double lo = (double)tmin * a, hi = (double)tmax * a;
+  double q = h - sq;
+  if (!(lo < q && q < hi)) {
+    q = h + sq;
+    if (!(lo < q && q < hi)) return false;
+  }
+  t_out = (float)(q / a);
+  return true;
+}
+RT_D bool hit_quad_rec(const F4 r[4], f3 o, f3 d, float tmin, float tmax, float& t_out,
+                       float& a_out, float& b_out) {
+  const F4 Q = r[0], N = r[1], A = r[2], B = r[3];
+  f3 n = xyz(N);
+  float denom = dot(n, d);
+  if (fabsf(denom) < 1e-8f) return false;
+  float t = (N.w - dot(n, o)) * rcp(denom);
+  if (!(tmin <= t && t <= tmax)) return false;
+  f3 pp = (o + d * t) - xyz(Q);
+  float alpha = dot(pp, xyz(A));
+  float beta = dot(pp, xyz(B));
+  if (!(0.0f <= alpha && alpha <= 1.0f) || !(0.0f <= beta && beta <= 1.0f)) return false;
+  t_out = t;
+  a_out = alpha;
+  b_out = beta;
+  return true;
+}
+RT_D bool hit_tri_rec(const F4 r[4], f3 o, f3 d, float tmin, float tmax, float& t_out,
+                      float& u_out, float& v_out) {
+  const F4 V0 = r[0], E0 = r[1], E1 = r[2];
+  f3 e0 = xyz(E0), e1 = xyz(E1);
+  f3 pvec = cross(d, e1);
+  float det = dot(e0, pvec);
+  if (fabsf(det) < 1e-8f) return false;
+  float inv = rcp(det);
+  f3 tvec = o - xyz(V0);
+  float u = dot(tvec, pvec) * inv;
+  if (u < 0.0f || u > 1.0f) return false;
+  f3 qvec = cross(tvec, e0);
+  float v = dot(d, qvec) * inv;
+  if (v < 0.0f || (u + v) > 1.0f) return false;
+  float t = dot(e1, qvec) * inv;
+  if (t < tmin || t > tmax) return false;
+  t_out = t;
+  u_out = u;
+  v_out = v;
+  return true;
+}
+RT_D bool hit_record(const F4 r[4], f3 o, f3 d, float time, float tmin, float tmax, float& t,
+                     float& u, float& v, uint32_t& ref) {
+  ref = fbits(r[0].w);
+  const uint32_t type = ref >> 30;
+  if (type == PRIM_QUAD) return hit_quad_rec(r, o, d, tmin, tmax, t, u, v);
+  if (type == PRIM_TRI) return hit_tri_rec(r, o, d, tmin, tmax, t, u, v);
+  u = v = 0.0f;
+  return hit_sphere_rec(r, o, d, time, tmin, tmax, t);
 }
 
 // same, with fp64 interval bounds and result (medium boundaries: the reference

@@ -8,7 +8,9 @@
 
 namespace rt {
 
-constexpr int kLdsNodes = 512;   // BVH nodes staged in LDS per workgroup (32 KB)
+constexpr int kLdsNodes = 384;   // 64-B slots staged in LDS per workgroup (24 KB): BVH nodes,
+                                 // then the leaf records when both fit (LDS instantiation)
+constexpr int kLdsW = 4;         // clamp-weight stack entries per lane kept in LDS (fused)
 constexpr int kStack = 64;       // traversal stack entries per lane (LDS short stack + HBM overflow)
 constexpr int kShortStack = 12;  // LDS entries per lane (column layout: [entry][thread])
 constexpr int kMaxIt = 1 << 16;  // per-iteration counter slots (no per-iteration memsets)
@@ -22,11 +24,24 @@ struct Counters {
   unsigned long long pushes;
   uint32_t chunk_head;
   uint32_t _pad[13];
+  unsigned long long prof[16];  // RT_PHASE_CLOCKS instrumentation
   uint32_t cnt[kMaxIt][kXcd];  // per-XCD queue lengths entering iteration i
 };
 
+// Division by a launch-invariant divisor: q = (t + ((n - t) >> s1)) >> s2 with
+// t = mulhi(m, n) (round-up magic, exact for all 32-bit n and d >= 1; host side
+// make_fastdiv in rt_render.hip; Hacker's Delight 10-8 with the add fix-up).
+struct FastDiv {
+  uint32_t m, s1, s2, d;
+};
+RT_D uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  const uint32_t t = __umulhi(f.m, n);
+  return (t + ((n - t) >> f.s1)) >> f.s2;
+}
+
 struct Params {
   DevScene sc;
+  FastDiv fd_npix, fd_width, fd_s;
   // camera (initialize camera.go:179-253, converted to fp32)
   float p00r[3], du[3], dv[3], cc[3], dku[3], dkv[3];  // p00r = pixel00 - center
   float bg[3];
@@ -77,9 +92,9 @@ struct Ids {
 };
 RT_D Ids chunk_ids(const Params& P, uint32_t chunk) {
   Ids r;
-  r.lpix = chunk % P.npix;
-  uint32_t sub = chunk / P.npix;
-  uint32_t row_l = r.lpix / (uint32_t)P.width;
+  uint32_t sub = fdiv(chunk, P.fd_npix);
+  r.lpix = chunk - sub * P.npix;
+  uint32_t row_l = fdiv(r.lpix, P.fd_width);
   r.col = r.lpix - row_l * (uint32_t)P.width;
   r.row = row_l * (uint32_t)P.nranks + (uint32_t)P.rank;
   r.gpix = r.row * (uint32_t)P.width + r.col;
@@ -91,7 +106,7 @@ RT_D Ids chunk_ids(const Params& P, uint32_t chunk) {
 // getRay camera.go:256-270 + sampleSquareStratified :277-282 + defocusDiskSample :285-290
 RT_D void camera_ray(const Params& P, const Ids& id, uint32_t sample, f3& o, f3& d, float& time) {
   rt_u32x4 r = rt_rng_draw(P.seed, id.gpix, sample, RT_STREAM_CAMERA);
-  uint32_t si = sample / (uint32_t)P.s, sj = sample - si * (uint32_t)P.s;
+  uint32_t si = fdiv(sample, P.fd_s), sj = sample - si * (uint32_t)P.s;
   float px = (((float)sj + rt_unit_f(r.v[0])) * P.recip_s) - 0.5f;
   float py = (((float)si + rt_unit_f(r.v[1])) * P.recip_s) - 0.5f;
   float fx = (float)id.col + px, fy = (float)id.row + py;
@@ -134,28 +149,61 @@ RT_D void slab(const F4& lo, const F4& hi, f3 o, f3 inv, float tmin, float tmax,
 // mixing both sources in one loop makes hipcc merge them into flat loads.
 // The traversal stack lives in LDS (kShortStack entries per lane, one column
 // per thread: conflict-free ds_read/write_b32) and overflows to HBM.
+// Explicit address spaces: with generic pointers hipcc selects between the two
+// bases and emits a flat load (slower, counts against both vmcnt and lgkmcnt).
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(1))) uint32_t glb_u32;
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4f lds_v4;
+typedef __attribute__((address_space(1))) v4f glb_v4;
+RT_D F4 ld_lds(const F4* p) {
+  const v4f v = *(const lds_v4*)p;
+  return {v.x, v.y, v.z, v.w};
+}
+RT_D F4 ld_glb(const F4* p) {
+  const v4f v = *(const glb_v4*)p;
+  return {v.x, v.y, v.z, v.w};
+}
+RT_D void st_lds(F4* p, F4 v) { *(lds_v4*)p = v4f{v.x, v.y, v.z, v.w}; }
+RT_D void st_glb(F4* p, F4 v) { *(glb_v4*)p = v4f{v.x, v.y, v.z, v.w}; }
 struct TravStack {
   uint32_t* lds;     // &lds_stack[0][threadIdx.x], stride blockDim.x
   uint32_t* ovf;     // &ostack[slot], stride cols
   uint32_t cols;
   RT_D void push(int sp, uint32_t v) const {
-    if (sp < kShortStack) lds[sp * 256] = v;
-    else ovf[(size_t)(sp - kShortStack) * cols] = v;
+    if (sp < kShortStack) ((lds_u32*)lds)[sp * 256] = v;
+    else ((glb_u32*)ovf)[(size_t)(sp - kShortStack) * cols] = v;
   }
   RT_D uint32_t pop(int sp) const {
-    return sp < kShortStack ? lds[sp * 256] : ovf[(size_t)(sp - kShortStack) * cols];
+    uint32_t v;
+    if (sp < kShortStack) v = ((lds_u32*)lds)[sp * 256];
+    else v = ((glb_u32*)ovf)[(size_t)(sp - kShortStack) * cols];
+    return v;
   }
 };
 
+#ifdef RT_PHASE_CLOCKS
+struct TravProf {
+  uint32_t inner, leaf, prims;
+};
+#define RT_TPROF(x) (x)
+#else
+struct TravProf {};
+#define RT_TPROF(x)
+#endif
+
+// LDS instantiation: lnodes holds the node array and, when recs_lds, the leaf
+// records right after it (uniform flag: both load forms exist, one runs)
 template <bool LDS>
-RT_D void trace_world(const DevScene& sc, const F4* lnodes, const TravStack& stack, f3 o, f3 d,
-                      float time, float tmin, Hit& best) {
+RT_D void trace_world(const DevScene& sc, const F4* lnodes, bool recs_lds, const TravStack& stack,
+                      f3 o, f3 d, float time, float tmin, Hit& best, TravProf& tp) {
   if (sc.root == PRIM_NONE) return;
-  f3 inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  f3 inv = mk3(rcp(d.x), rcp(d.y), rcp(d.z));
   int sp = 0;
   uint32_t cur = sc.root;
   for (;;) {
     if (!(cur & LEAF_BIT)) {
+      RT_TPROF(++tp.inner);
       const F4* g = LDS ? lnodes + 4 * cur : sc.nodes + 4 * (size_t)cur;
       const F4 a0 = g[0], a1 = g[1], b0 = g[2], b1 = g[3];
       bool h0, h1;
@@ -179,10 +227,22 @@ RT_D void trace_world(const DevScene& sc, const F4* lnodes, const TravStack& sta
       }
     } else {
       uint32_t first = (cur >> 4) & 0x7FFFFFFu, count = (cur & 15u) + 1u;
+      RT_TPROF(++tp.leaf);
+      RT_TPROF(tp.prims += count);
+      // leaf records are contiguous: no ref indirection, all four loads issue at once
       for (uint32_t k = 0; k < count; ++k) {
-        uint32_t ref = sc.refs[first + k];
+        const uint32_t ri = 4 * (first + k);
+        F4 rec[4];
+        if (LDS && recs_lds) {
+          const F4* q = lnodes + 4 * sc.n_nodes + ri;
+          for (int e = 0; e < 4; ++e) rec[e] = ld_lds(q + e);
+        } else {
+          const F4* q = sc.leafprims + ri;
+          for (int e = 0; e < 4; ++e) rec[e] = ld_glb(q + e);
+        }
         float t, u, v;
-        if (hit_prim(sc, ref, o, d, time, tmin, best.t, t, u, v)) {
+        uint32_t ref;
+        if (hit_record(rec, o, d, time, tmin, best.t, t, u, v, ref)) {
           best.t = t;
           best.u = u;
           best.v = v;
@@ -410,7 +470,7 @@ RT_D f3 lights_random(const DevScene& sc, f3 origin, const rt_u32x4& r) {
 }
 
 RT_D void flush_chunk(const Params& P, uint32_t chunk, f3 acc) {
-  const uint32_t lp = chunk % P.npix;
+  const uint32_t lp = chunk - fdiv(chunk, P.fd_npix) * P.npix;
   const float c[3] = {acc.x, acc.y, acc.z};
   for (int ch = 0; ch < 3; ++ch) {
     float v = c[ch];
@@ -466,6 +526,25 @@ RT_D void set_acc(const Params& P, uint32_t slot, Path& s, f3 v) {
   else s.acc = v;
 }
 
+// Clamp-weight stack: entries below nlds in an LDS column (fused kernel, one
+// per thread), the rest in HBM [entry - nlds][slot].  LDS keeps the common
+// shallow pushes off the vector-memory counter (a store holds vmcnt for
+// hundreds of cycles and every later load waits behind it).
+struct WStack {
+  F4* lds;  // &lds_w[0][threadIdx.x], stride 256
+  int nlds;
+  RT_D void put(const Params& P, uint32_t slot, uint32_t k, F4 v) const {
+    if ((int)k < nlds) st_lds(lds + k * 256, v);
+    else st_glb(P.stack + (size_t)(k - nlds) * P.P + slot, v);
+  }
+  RT_D F4 get(const Params& P, uint32_t slot, uint32_t k) const {
+    F4 v;
+    if ((int)k < nlds) v = ld_lds(lds + k * 256);
+    else v = ld_glb(P.stack + (size_t)(k - nlds) * P.P + slot);
+    return v;
+  }
+};
+
 template <bool SOA>
 RT_D void store_ray(const Params& P, uint32_t slot, const Path& s) {
   if (SOA) {
@@ -504,7 +583,7 @@ RT_D void start_sample(const Params& P, uint32_t slot, Path& s, uint32_t chunk, 
 // One vertex of rayColor (camera.go:293-331) given its closest hit.
 // Returns OUT_ALIVE (continue with s.o/s.d), or OUT_NEED_CHUNK (chunk flushed).
 template <bool SOA>
-RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h) {
+RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const WStack& ws) {
   const DevScene& sc = P.sc;
   const f3 o = s.o, d = s.d;
   const float time = s.time;
@@ -617,14 +696,14 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h) {
           spdf = ct < 0.0f ? 0.0f : ct / kPi;
         }
         float pdf = 0.5f * lights_pdf(sc, p, ndir) + 0.5f * bsdf_pdf;
-        weight = (att * spdf) * (1.0f / pdf);
+        weight = (att * spdf) * rcp(pdf);
         clamp_vertex = true;
       }
       // vertex bookkeeping (H1: the clamp is folded backwards at termination)
       if (clamp_vertex) {
         if (s.flags & F_PEND) {
           f3 pv = get_pend<SOA>(P, slot, s);
-          P.stack[(size_t)s.nst * P.P + slot] = {pv.x, pv.y, pv.z, 0.0f};
+          ws.put(P, slot, s.nst, {pv.x, pv.y, pv.z, 0.0f});
           ++s.nst;
           ++s.pushes;
         }
@@ -656,7 +735,7 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h) {
   if (!(zero && !(s.flags & F_NONFINITE))) {
     if (s.flags & F_PEND) L = clamp_contribution(get_pend<SOA>(P, slot, s) * L, P.maxc);
     for (int kk = (int)s.nst - 1; kk >= 0; --kk)
-      L = clamp_contribution(xyz(P.stack[(size_t)kk * P.P + slot]) * L, P.maxc);
+      L = clamp_contribution(xyz(ws.get(P, slot, (uint32_t)kk)) * L, P.maxc);
     if (s.flags & F_PRE) L = get_pre<SOA>(P, slot, s) * L;
   } else {
     L = mk3(0, 0, 0);

@@ -30,11 +30,17 @@
 
 namespace rt {
 
-// the whole BVH node array -> LDS (only used when n_nodes <= kLdsNodes)
-RT_D void stage_nodes(const Params& P, F4* lnodes) {
+// the whole BVH node array -> LDS (only used when n_nodes <= kLdsNodes), then
+// the leaf records when they fit too; returns whether they did
+RT_D bool stage_nodes(const Params& P, F4* lnodes) {
   const int nl = min(P.sc.n_nodes, kLdsNodes);
   for (int i = threadIdx.x; i < 4 * nl; i += blockDim.x) lnodes[i] = P.sc.nodes[i];
+  const bool recs = P.sc.n_nodes + P.sc.n_refs <= kLdsNodes;
+  if (recs)
+    for (int i = threadIdx.x; i < 4 * P.sc.n_refs; i += blockDim.x)
+      lnodes[4 * nl + i] = P.sc.leafprims[i];
   __syncthreads();
+  return recs;
 }
 
 RT_D void record_trace(const Params& P, const Path& s, const Hit& best) {
@@ -48,9 +54,10 @@ RT_D void record_trace(const Params& P, const Path& s, const Hit& best) {
 
 // closest hit of one path (world BVH + media), camera.go:300
 template <bool LDS>
-RT_D Hit intersect(const Params& P, const F4* lnodes, const TravStack& ts, const Path& s) {
+RT_D Hit intersect(const Params& P, const F4* lnodes, bool recs_lds, const TravStack& ts,
+                   const Path& s, TravProf& tp) {
   Hit best = {kInf, 0.0f, 0.0f, PRIM_NONE};
-  trace_world<LDS>(P.sc, lnodes, ts, s.o, s.d, s.time, 0.001f, best);
+  trace_world<LDS>(P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, best, tp);
   if (P.sc.n_media > 0) {
     const Ids id = chunk_ids(P, s.chunk);
     trace_media(P, s.o, s.d, s.time, 0.001f, id.gpix, id.sample0 + s.j, s.k, best);
@@ -75,7 +82,7 @@ template <bool LDS>
 __global__ __launch_bounds__(256) void k_extend(Params P, int it) {
   __shared__ F4 lnodes[LDS ? 4 * kLdsNodes : 4];
   __shared__ uint32_t lstack[kShortStack * 256];
-  if (LDS) stage_nodes(P, lnodes);
+  const bool recs_lds = LDS && stage_nodes(P, lnodes);
   const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
   const TravStack ts = {&lstack[threadIdx.x], P.ostack + gtid, P.stack_cols};
   const uint32_t sel = (uint32_t)it & 1u;
@@ -91,7 +98,8 @@ __global__ __launch_bounds__(256) void k_extend(Params P, int it) {
     const uint32_t slot = queue_slot(P, q, cnt, i);
     Path s;
     load_path(P, slot, s);
-    const Hit best = intersect<LDS>(P, lnodes, ts, s);
+    TravProf tp{};
+    const Hit best = intersect<LDS>(P, lnodes, recs_lds, ts, s, tp);
     P.hit[slot] = {best.t, best.u, best.v, bitsf(best.ref)};
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&P.ctr->segments, (unsigned long long)n);
@@ -115,7 +123,8 @@ __global__ __launch_bounds__(256) void k_shade(Params P, int it) {
     load_path(P, slot, s);
     const F4 hv = P.hit[slot];
     const Hit h = {hv.x, hv.y, hv.z, fbits(hv.w)};
-    int out = shade_core<true>(P, slot, s, h);
+    const WStack ws = {nullptr, 0};  // the weight stack outlives the launch: HBM only
+    int out = shade_core<true>(P, slot, s, h, ws);
     if (out == OUT_NEED_CHUNK) {
       // static work split: slot s renders chunks s, s+P, s+2P, ... (no atomics)
       const uint32_t c = s.chunk + P.P;
@@ -166,14 +175,29 @@ template <bool LDS, int WAVES>
 __global__ __launch_bounds__(256, WAVES) void k_fused(Params P) {
   __shared__ F4 lnodes[LDS ? 4 * kLdsNodes : 4];
   __shared__ uint32_t lstack[kShortStack * 256];
-  if (LDS) stage_nodes(P, lnodes);
+  __shared__ F4 lw[kLdsW * 256];
+  const bool recs_lds = LDS && stage_nodes(P, lnodes);
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;  // weight-stack column
   const TravStack ts = {&lstack[threadIdx.x], P.ostack + slot, P.stack_cols};
+  const WStack ws = {&lw[threadIdx.x], kLdsW};
   Path s;
   s.segs = 0;
   s.pushes = 0;
   bool has = false;
   WaveBatch b = {0u, 0u};
+#ifdef RT_PHASE_CLOCKS
+  // per-wave phase clocks and SIMD-utilisation counters (profiling build only)
+  unsigned long long pc[16] = {};
+  unsigned long long tw0 = wall_clock64(), ck = clock64();
+#define RT_PHASE(i)                      \
+  do {                                   \
+    const unsigned long long n_ = clock64(); \
+    pc[i] += n_ - ck;                    \
+    ck = n_;                             \
+  } while (0)
+#else
+#define RT_PHASE(i)
+#endif
   for (;;) {
     const uint32_t c = grab_chunk(P, b, !has);
     if (c != 0xFFFFFFFFu) {
@@ -181,12 +205,37 @@ __global__ __launch_bounds__(256, WAVES) void k_fused(Params P) {
       has = true;
     }
     if (!__any(has)) break;
+    RT_PHASE(0);
     if (has) {
-      const Hit best = intersect<LDS>(P, lnodes, ts, s);
+      TravProf tp{};
+      const Hit best = intersect<LDS>(P, lnodes, recs_lds, ts, s, tp);
+#ifdef RT_PHASE_CLOCKS
+      RT_PHASE(1);
+      const unsigned long long act = __ballot(1);
+      pc[3] += 1;
+      pc[4] += __popcll(act);
+      uint32_t mi = tp.inner, ml = tp.leaf, si = tp.inner, sl = tp.leaf, sp = tp.prims, mp = tp.prims;
+      for (int off = 32; off > 0; off >>= 1) {
+        mi = max(mi, (uint32_t)__shfl_xor((int)mi, off));
+        ml = max(ml, (uint32_t)__shfl_xor((int)ml, off));
+        mp = max(mp, (uint32_t)__shfl_xor((int)mp, off));
+        si += __shfl_xor(si, off);
+        sl += __shfl_xor(sl, off);
+        sp += __shfl_xor(sp, off);
+      }
+      pc[5] += mi; pc[6] += si; pc[7] += ml; pc[8] += sl; pc[9] += mp; pc[10] += sp;
+      ck = clock64();
+#endif
       ++s.segs;
-      if (shade_core<false>(P, slot, s, best) == OUT_NEED_CHUNK) has = false;
+      if (shade_core<false>(P, slot, s, best, ws) == OUT_NEED_CHUNK) has = false;
     }
+    RT_PHASE(2);
   }
+#ifdef RT_PHASE_CLOCKS
+  pc[11] = wall_clock64() - tw0;
+  if (lane_id() == 0)
+    for (int i = 0; i < 12; ++i) atomicAdd(&P.ctr->prof[i], pc[i]);
+#endif
   uint32_t segs = s.segs, pushes = s.pushes;
   for (int off = 32; off > 0; off >>= 1) {
     segs += __shfl_xor(segs, off);
@@ -284,6 +333,49 @@ static int upload(DeviceScene* ds, const std::vector<T>& v, const T** out) {
   return RT_OK;
 }
 
+static FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f{1u, 0u, 0u, d};
+  if (d <= 1) return f;  // d == 1: t = 0, q = n
+  const uint32_t l = 32u - (uint32_t)__builtin_clz(d - 1u);
+  f.m = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - d)) / d + 1u);
+  f.s1 = 1u;
+  f.s2 = l - 1u;
+  return f;
+}
+
+// the traversal's leaf records (rt_device.h "leaf records"), in refs order
+static void build_leaf_records(const HostScene& h, std::vector<F4>& recs) {
+  recs.assign(4 * h.refs.size(), F4{0, 0, 0, 0});
+  for (size_t i = 0; i < h.refs.size(); ++i) {
+    const uint32_t ref = h.refs[i], type = ref >> 30, idx = ref & 0x3FFFFFFFu;
+    F4* r = &recs[4 * i];
+    float rb;
+    memcpy(&rb, &ref, 4);
+    if (type == PRIM_SPHERE) {
+      const F4 cr = h.sph_cr[idx], mv = h.sph_mv[idx];
+      r[0] = {cr.x, cr.y, cr.z, rb};
+      r[1] = {mv.x, mv.y, mv.z, cr.w};
+    } else if (type == PRIM_QUAD) {
+      const F4* q = &h.quad[5 * (size_t)idx];  // Q|D, u|area, v|mat, n, w
+      const double u[3] = {q[1].x, q[1].y, q[1].z}, v[3] = {q[2].x, q[2].y, q[2].z},
+                   w[3] = {q[4].x, q[4].y, q[4].z};
+      auto cr = [](const double* a, const double* b, int k) {
+        return k == 0 ? a[1] * b[2] - a[2] * b[1] : k == 1 ? a[2] * b[0] - a[0] * b[2]
+                                                           : a[0] * b[1] - a[1] * b[0];
+      };
+      r[0] = {q[0].x, q[0].y, q[0].z, rb};
+      r[1] = {q[3].x, q[3].y, q[3].z, q[0].w};
+      r[2] = {(float)cr(v, w, 0), (float)cr(v, w, 1), (float)cr(v, w, 2), 0.0f};
+      r[3] = {(float)cr(w, u, 0), (float)cr(w, u, 1), (float)cr(w, u, 2), 0.0f};
+    } else {
+      const F4* t = &h.tri[3 * (size_t)idx];  // v0|mat, e0|area, e1|flags
+      r[0] = {t[0].x, t[0].y, t[0].z, rb};
+      r[1] = {t[1].x, t[1].y, t[1].z, 0.0f};
+      r[2] = {t[2].x, t[2].y, t[2].z, 0.0f};
+    }
+  }
+}
+
 static int ensure_scene(Scene* s, int device) {
   if (s->dev && s->dev->device == device) return RT_OK;
   delete s->dev;
@@ -321,6 +413,11 @@ static int ensure_scene(Scene* s, int device) {
   UP(h.tri_attr, tri_attr);
   UP(h.nodes, nodes);
   UP(h.refs, refs);
+  {
+    std::vector<F4> recs;
+    build_leaf_records(h, recs);
+    UP(recs, leafprims);
+  }
   UP(h.media, media);
   UP(h.medium_refs, medium_refs);
   UP(h.lights, lights);
@@ -335,6 +432,7 @@ static int ensure_scene(Scene* s, int device) {
   d.n_media = (int32_t)h.media.size();
   d.medium_draws = h.medium_draws;
   d.n_lights = (int32_t)h.lights.size();
+  d.n_refs = (int32_t)h.refs.size();
   return RT_OK;
 }
 
@@ -502,6 +600,9 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   p.n_chunks = n_chunks;
   p.P = P;
   p.ss = ss;
+  p.fd_npix = make_fastdiv(npix);
+  p.fd_width = make_fastdiv(W);
+  p.fd_s = make_fastdiv((uint32_t)cd.spp_sqrt);
   p.seed = o.seed;
   p.ray_o = st->ray_o;
   p.ray_d = st->ray_d;
@@ -625,6 +726,13 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     Counters hc;
     HIP_OK(hipMemcpy(&hc, st->ctr, offsetof(Counters, cnt), hipMemcpyDeviceToHost));
     stats->samples = (uint64_t)npix * ss;
+#ifdef RT_PHASE_CLOCKS
+    fprintf(stderr,
+            "[rt phase] grab %llu isect %llu shade %llu | iters %llu active_lanes %llu | "
+            "inner max %llu sum %llu | leaf max %llu sum %llu | prims max %llu sum %llu | wall %llu\n",
+            hc.prof[0], hc.prof[1], hc.prof[2], hc.prof[3], hc.prof[4], hc.prof[5], hc.prof[6],
+            hc.prof[7], hc.prof[8], hc.prof[9], hc.prof[10], hc.prof[11]);
+#endif
     stats->segments = hc.segments;
     stats->stack_pushes = hc.pushes;
     stats->extend_rays = hc.segments;
