@@ -24,6 +24,8 @@ RT_NOISE_PERLIN, RT_NOISE_MARBLE, RT_NOISE_TURBULENT = 1, 2, 3
 (RT_NODE_LIST, RT_NODE_BVH, RT_NODE_SPHERE, RT_NODE_QUAD, RT_NODE_TRIANGLE,
  RT_NODE_TRANSLATE, RT_NODE_ROTATE_Y, RT_NODE_MEDIUM) = range(8)
 RT_FLAG_PROFILE = 1
+RT_FT_SPHERE, RT_FT_TRI, RT_FT_METAL, RT_FT_DIEL = 1, 2, 4, 8
+RT_FT_MEDIA, RT_FT_CHECKER, RT_FT_IMAGE, RT_FT_NOISE = 16, 32, 64, 128
 RT_MODE_AUTO, RT_MODE_WAVEFRONT, RT_MODE_FUSED = 0, 1, 2
 
 D3 = C.c_double * 3
@@ -57,7 +59,7 @@ class RtSceneInfo(C.Structure):
         "n_spheres", "n_quads", "n_triangles", "n_world_prims", "n_media",
         "n_lights", "n_bvh_nodes", "bvh_depth", "max_leaf", "n_materials",
         "n_textures", "n_images", "n_perlins", "medium_draws")] + [
-        ("device_bytes", C.c_int64)]
+        ("device_bytes", C.c_int64), ("features", C.c_int32), ("_pad", C.c_int32)]
 
 
 class RtRenderOpts(C.Structure):
@@ -80,6 +82,7 @@ class RtStats(C.Structure):
         ("n_shade_launches", C.c_int32), ("iterations", C.c_int32),
         ("rows", C.c_int32), ("mode", C.c_int32), ("path_slots", C.c_int32),
         ("ms_fused", C.c_double),
+        ("kernel_features", C.c_int32), ("scene_features", C.c_int32),
     ]
 
 

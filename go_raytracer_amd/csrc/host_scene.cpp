@@ -5,6 +5,36 @@
 
 using rt::set_error;
 
+namespace rt {
+// Prim types reachable by traversal, shading or light sampling, material kinds
+// and texture kinds present: selects the fused-kernel instantiation.
+uint32_t scene_features(const HostScene& h) {
+  uint32_t f = 0;
+  auto prim = [&f](uint32_t ref) {
+    if (ref == PRIM_NONE) return;
+    const uint32_t type = ref >> 30;
+    if (type == PRIM_SPHERE) f |= FT_SPHERE;
+    if (type == PRIM_TRI) f |= FT_TRI;
+    if (type == PRIM_MEDIUM) f |= FT_MEDIA;
+  };
+  for (uint32_t r : h.refs) prim(r);
+  for (uint32_t r : h.medium_refs) prim(r);
+  for (const DevLight& l : h.lights) prim(l.ref);
+  if (!h.media.empty()) f |= FT_MEDIA;
+  for (const DevMaterial& m : h.mats) {
+    if (m.kind == RT_MAT_METAL) f |= FT_METAL;
+    if (m.kind == RT_MAT_DIELECTRIC) f |= FT_DIEL;
+    if (m.kind == RT_MAT_ISOTROPIC) f |= FT_MEDIA;
+  }
+  for (const DevTexture& t : h.texs) {
+    if (t.kind == RT_TEX_CHECKER) f |= FT_CHECKER;
+    if (t.kind == RT_TEX_IMAGE) f |= FT_IMAGE;
+    if (t.kind == RT_TEX_NOISE) f |= FT_NOISE;
+  }
+  return f;
+}
+}  // namespace rt
+
 extern "C" {
 
 int rt_scene_create(const rt_tree* t, int world, int lights, rt_scene** out) {
@@ -55,6 +85,7 @@ int rt_scene_info_get(const rt_scene* sc, rt_scene_info* o) {
   b += h.texs.size() * sizeof(rt::DevTexture) + h.texels.size();
   b += h.images.size() * sizeof(rt::DevImage) + h.perlins.size() * sizeof(rt::DevPerlin);
   o->device_bytes = b;
+  o->features = (int32_t)rt::scene_features(h);
   return RT_OK;
 }
 

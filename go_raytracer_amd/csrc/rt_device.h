@@ -50,6 +50,16 @@ enum : uint32_t { TRI_HAS_NORMALS = 1u, TRI_HAS_UV = 2u };
 //           quad.Hit objects.go:186-187 with the cross products hoisted)
 //  tri:    v0.xyz | ref       ;  e0.xyz | 0           ; e1.xyz | 0 ; 0
 
+// ---- scene features: the fused kernel is instantiated per feature set so that
+// code a scene cannot reach (and its register pressure) is compiled out.
+// Quads, Lambertian, diffuse lights and solid textures are always supported.
+enum : uint32_t {
+  FT_SPHERE = 1u, FT_TRI = 2u, FT_METAL = 4u, FT_DIEL = 8u,
+  FT_MEDIA = 16u,   // constant media or isotropic materials
+  FT_CHECKER = 32u, FT_IMAGE = 64u, FT_NOISE = 128u,
+  FT_ALL = 255u
+};
+
 struct DevMedium {           // constantMedium medium.go:13-18
   uint32_t bfirst, bcount;   // boundary prim refs in medium_refs
   float neg_inv_density;     // -1/rho

@@ -76,6 +76,8 @@ int flatten_scene(const Tree& t, int world, int lights, HostScene& out);
 // host_bvh.cpp
 int build_bvh(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi,
               const std::vector<uint32_t>& prims);
+// host_scene.cpp: RT_FT_* features a flattened scene needs
+uint32_t scene_features(const HostScene& h);
 // rt_render.hip
 void release_device(Scene* s);
 

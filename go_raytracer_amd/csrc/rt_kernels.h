@@ -247,12 +247,15 @@ RT_D bool hit_tri_rec(const F4 r[4], f3 o, f3 d, float tmin, float tmax, float& 
   v_out = v;
   return true;
 }
+#define HAS(f) ((FT & (f)) != 0u)
+template <uint32_t FT>
 RT_D bool hit_record(const F4 r[4], f3 o, f3 d, float time, float tmin, float tmax, float& t,
                      float& u, float& v, uint32_t& ref) {
   ref = fbits(r[0].w);
   const uint32_t type = ref >> 30;
-  if (type == PRIM_QUAD) return hit_quad_rec(r, o, d, tmin, tmax, t, u, v);
-  if (type == PRIM_TRI) return hit_tri_rec(r, o, d, tmin, tmax, t, u, v);
+  if (!HAS(FT_SPHERE | FT_TRI) || type == PRIM_QUAD) return hit_quad_rec(r, o, d, tmin, tmax, t, u, v);
+  if (HAS(FT_TRI) && (!HAS(FT_SPHERE) || type == PRIM_TRI))
+    return hit_tri_rec(r, o, d, tmin, tmax, t, u, v);
   u = v = 0.0f;
   return hit_sphere_rec(r, o, d, time, tmin, tmax, t);
 }

@@ -194,7 +194,7 @@ struct TravProf {};
 
 // LDS instantiation: lnodes holds the node array and, when recs_lds, the leaf
 // records right after it (uniform flag: both load forms exist, one runs)
-template <bool LDS>
+template <bool LDS, uint32_t FT>
 RT_D void trace_world(const DevScene& sc, const F4* lnodes, bool recs_lds, const TravStack& stack,
                       f3 o, f3 d, float time, float tmin, Hit& best, TravProf& tp) {
   if (sc.root == PRIM_NONE) return;
@@ -242,7 +242,7 @@ RT_D void trace_world(const DevScene& sc, const F4* lnodes, bool recs_lds, const
         }
         float t, u, v;
         uint32_t ref;
-        if (hit_record(rec, o, d, time, tmin, best.t, t, u, v, ref)) {
+        if (hit_record<FT>(rec, o, d, time, tmin, best.t, t, u, v, ref)) {
           best.t = t;
           best.u = u;
           best.v = v;
@@ -342,17 +342,18 @@ RT_D float perlin_turb(const DevPerlin& pl, f3 p, int depth) {  // perlin.go:57-
   return fabsf(accum);
 }
 
+template <uint32_t FT>
 RT_D f3 tex_value(const DevScene& sc, int tex, float u, float v, f3 p) {
   for (int guard = 0; guard < 64; ++guard) {
     const DevTexture T = sc.texs[tex];
-    if (T.kind == RT_TEX_SOLID) return xyz(T.color);
-    if (T.kind == RT_TEX_CHECKER) {  // texture.go:50-60
+    if (!HAS(FT_CHECKER | FT_IMAGE | FT_NOISE) || T.kind == RT_TEX_SOLID) return xyz(T.color);
+    if (HAS(FT_CHECKER) && T.kind == RT_TEX_CHECKER) {  // texture.go:50-60
       float inv = T.color.w;
       int x = (int)floorf(inv * p.x), y = (int)floorf(inv * p.y), z = (int)floorf(inv * p.z);
       tex = ((x + y + z) % 2 == 0) ? T.a : T.b;
       continue;
     }
-    if (T.kind == RT_TEX_IMAGE) {  // texture.go:70-86 + PixelData imageLoader.go:52-62
+    if (HAS(FT_IMAGE) && (!HAS(FT_NOISE) || T.kind == RT_TEX_IMAGE)) {  // texture.go:70-86 + PixelData imageLoader.go:52-62
       const DevImage im = sc.images[T.a];
       if (im.h <= 0) return mk3(0, 1, 1);
       float uu = fabsf(fmodf(u, 1.0f));
@@ -367,6 +368,7 @@ RT_D f3 tex_value(const DevScene& sc, int tex, float u, float v, f3 p) {
       const float s = 1.0f / 255.0f;
       return mk3((float)px[0] * s, (float)px[1] * s, (float)px[2] * s);
     }
+    if (!HAS(FT_NOISE)) return mk3(0, 0, 0);
     // noise, texture.go:112-125
     const DevPerlin& pl = sc.perlins[T.a];
     float scale = T.color.w;
@@ -395,9 +397,10 @@ RT_D f3 tri_normal(const DevScene& sc, uint32_t idx, float bu, float bv) {
 }
 
 // light PdfValue: sphere objects.go:52-62, quad :152-160, triangle :356-367
+template <uint32_t FT>
 RT_D float prim_pdf(const DevScene& sc, uint32_t ref, f3 origin, f3 dir) {
   uint32_t type = ref >> 30, idx = ref & 0x3FFFFFFFu;
-  if (type == PRIM_SPHERE) {
+  if (HAS(FT_SPHERE) && type == PRIM_SPHERE) {
     float t;
     if (!hit_sphere(sc, idx, origin, dir, 0.0f, 0.0001f, kInf, t)) return 0.0f;
     const F4 cr = sc.sph_cr[idx];
@@ -408,7 +411,7 @@ RT_D float prim_pdf(const DevScene& sc, uint32_t ref, f3 origin, f3 dir) {
   }
   float t, u, v, area;
   f3 n;
-  if (type == PRIM_QUAD) {
+  if (!HAS(FT_TRI) || type == PRIM_QUAD) {
     if (!hit_quad(sc, idx, origin, dir, 0.001f, kInf, t, u, v)) return 0.0f;
     const F4* q = sc.quad + 5 * (size_t)idx;
     n = xyz(q[3]);
@@ -424,17 +427,19 @@ RT_D float prim_pdf(const DevScene& sc, uint32_t ref, f3 origin, f3 dir) {
 }
 
 // HittableList.PdfValue hittable.go:89-97 over the flattened light table
+template <uint32_t FT>
 RT_D float lights_pdf(const DevScene& sc, f3 origin, f3 dir) {
   float sum = 0.0f;
   for (int i = 0; i < sc.n_lights; ++i) {
     const DevLight L = sc.lights[i];
     if (L.ref == PRIM_NONE) continue;
-    sum += L.weight * prim_pdf(sc, L.ref, origin, dir);
+    sum += L.weight * prim_pdf<FT>(sc, L.ref, origin, dir);
   }
   return sum;
 }
 
 // HittableList.Random hittable.go:98-103 + sphere/quad/Triangle.Random
+template <uint32_t FT>
 RT_D f3 lights_random(const DevScene& sc, f3 origin, const rt_u32x4& r) {
   const float s0 = rt_unit_f(r.v[2]), s1 = rt_unit_f(r.v[3]);
   int lo = 0, hi = sc.n_lights - 1;
@@ -448,7 +453,7 @@ RT_D f3 lights_random(const DevScene& sc, f3 origin, const rt_u32x4& r) {
   const uint32_t ref = sc.lights[lo].ref;
   if (ref == PRIM_NONE) return mk3(rt_unit_f(r.v[1]), s0, s1);
   uint32_t type = ref >> 30, idx = ref & 0x3FFFFFFFu;
-  if (type == PRIM_SPHERE) {  // sphere.Random + randomToSphere objects.go:63-80
+  if (HAS(FT_SPHERE) && type == PRIM_SPHERE) {  // sphere.Random + randomToSphere objects.go:63-80
     const F4 cr = sc.sph_cr[idx];
     f3 dir = xyz(cr) - origin;
     float dist2 = dot(dir, dir);
@@ -457,7 +462,7 @@ RT_D f3 lights_random(const DevScene& sc, f3 origin, const rt_u32x4& r) {
     float tt = sqrtf(1.0f - z * z);  // phi = 2*pi*s0
     return onb_transform(b, mk3(cos2pi(s0) * tt, sin2pi(s0) * tt, z));
   }
-  if (type == PRIM_QUAD) {  // quad.Random objects.go:161-165
+  if (!HAS(FT_TRI) || type == PRIM_QUAD) {  // quad.Random objects.go:161-165
     const F4* q = sc.quad + 5 * (size_t)idx;
     return (xyz(q[0]) + xyz(q[1]) * s0 + xyz(q[2]) * s1) - origin;
   }
@@ -582,7 +587,7 @@ RT_D void start_sample(const Params& P, uint32_t slot, Path& s, uint32_t chunk, 
 
 // One vertex of rayColor (camera.go:293-331) given its closest hit.
 // Returns OUT_ALIVE (continue with s.o/s.d), or OUT_NEED_CHUNK (chunk flushed).
-template <bool SOA>
+template <bool SOA, uint32_t FT>
 RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const WStack& ws) {
   const DevScene& sc = P.sc;
   const f3 o = s.o, d = s.d;
@@ -602,14 +607,14 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
     int mat;
     bool ff = true;
     f3 n;
-    if (type == PRIM_SPHERE) {
+    if (HAS(FT_SPHERE) && type == PRIM_SPHERE) {
       const F4 cr = sc.sph_cr[idx], mv = sc.sph_mv[idx];
       f3 cc = xyz(cr) + xyz(mv) * time;
       nout = (p - cc) * (1.0f / cr.w);
       mat = (int)fbits(mv.w);
       ff = dot(d, nout) < 0;  // setFaceNormal hittable.go:27-34
       n = ff ? nout : -nout;
-      if (sc.mats[mat]._pad != 0.0f) {  // texture reads u,v: calculateSphereUV objects.go:44-50
+      if (HAS(FT_IMAGE) && sc.mats[mat]._pad != 0.0f) {  // texture reads u,v: calculateSphereUV objects.go:44-50
         const F2 rs = sc.sph_uv[idx];
         f3 no = mk3(rs.x * nout.x - rs.y * nout.z, nout.y, rs.y * nout.x + rs.x * nout.z);
         float theta = acosf(-no.y);
@@ -617,13 +622,13 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
         u = phi / (2.0f * kPi);
         v = theta / kPi;
       }
-    } else if (type == PRIM_QUAD) {
+    } else if (!HAS(FT_TRI | FT_MEDIA) || type == PRIM_QUAD) {
       const F4* q = sc.quad + 5 * (size_t)idx;
       nout = xyz(q[3]);
       mat = (int)fbits(q[2].w);
       ff = dot(d, nout) < 0;
       n = ff ? nout : -nout;
-    } else if (type == PRIM_TRI) {
+    } else if (HAS(FT_TRI) && (!HAS(FT_MEDIA) || type == PRIM_TRI)) {
       nout = tri_normal(sc, idx, u, v);
       mat = (int)fbits(sc.tri[3 * (size_t)idx].w);
       ff = dot(d, nout) < 0;
@@ -645,7 +650,7 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
     }
     const DevMaterial M = sc.mats[mat];
     if (M.kind == RT_MAT_DIFFUSE_LIGHT) {  // Emitted materials.go:150-155; Scatter false
-      lterm = ff ? tex_value(sc, M.tex, u, v, p) : mk3(0, 0, 0);
+      lterm = ff ? tex_value<FT>(sc, M.tex, u, v, p) : mk3(0, 0, 0);
       term = true;
     } else {
       const Ids id = chunk_ids(P, s.chunk);
@@ -653,11 +658,11 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
       f3 ndir;
       bool clamp_vertex = false;
       f3 weight;
-      if (M.kind == RT_MAT_METAL) {  // materials.go:70-79
+      if (HAS(FT_METAL) && M.kind == RT_MAT_METAL) {  // materials.go:70-79
         f3 refl = unit(reflect(d, n));
         ndir = refl + uniform_sphere(rt_unit_f(r.v[2]), rt_unit_f(r.v[3])) * M.param;
         weight = xyz(M.albedo);
-      } else if (M.kind == RT_MAT_DIELECTRIC) {  // materials.go:94-130
+      } else if (HAS(FT_DIEL) && M.kind == RT_MAT_DIELECTRIC) {  // materials.go:94-130
         float ior = M.param;
         float ri = ff ? 1.0f / ior : ior;
         f3 ud = unit(d);
@@ -674,12 +679,12 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
         ndir = refl ? reflect(ud, n) : refract(ud, n, ri);
         weight = mk3(1, 1, 1);
       } else {  // lambertian materials.go:45-57 / isotropic :157-177 + mixture pdf.go:58-74
-        const bool iso = M.kind == RT_MAT_ISOTROPIC;
-        f3 att = tex_value(sc, M.tex, u, v, p);
+        const bool iso = HAS(FT_MEDIA) && M.kind == RT_MAT_ISOTROPIC;
+        f3 att = tex_value<FT>(sc, M.tex, u, v, p);
         Onb b;
         if (!iso) b = make_onb(n);
         if (rt_unit_f(r.v[0]) < 0.5f) {
-          ndir = lights_random(sc, p, r);
+          ndir = lights_random<FT>(sc, p, r);
         } else if (iso) {
           ndir = uniform_sphere(rt_unit_f(r.v[2]), rt_unit_f(r.v[3]));
         } else {
@@ -695,7 +700,7 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
           float ct = dot(n, ud);
           spdf = ct < 0.0f ? 0.0f : ct / kPi;
         }
-        float pdf = 0.5f * lights_pdf(sc, p, ndir) + 0.5f * bsdf_pdf;
+        float pdf = 0.5f * lights_pdf<FT>(sc, p, ndir) + 0.5f * bsdf_pdf;
         weight = (att * spdf) * rcp(pdf);
         clamp_vertex = true;
       }

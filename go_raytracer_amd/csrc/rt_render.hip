@@ -53,12 +53,12 @@ RT_D void record_trace(const Params& P, const Path& s, const Hit& best) {
 }
 
 // closest hit of one path (world BVH + media), camera.go:300
-template <bool LDS>
+template <bool LDS, uint32_t FT>
 RT_D Hit intersect(const Params& P, const F4* lnodes, bool recs_lds, const TravStack& ts,
                    const Path& s, TravProf& tp) {
   Hit best = {kInf, 0.0f, 0.0f, PRIM_NONE};
-  trace_world<LDS>(P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, best, tp);
-  if (P.sc.n_media > 0) {
+  trace_world<LDS, FT>(P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, best, tp);
+  if (HAS(FT_MEDIA) && P.sc.n_media > 0) {
     const Ids id = chunk_ids(P, s.chunk);
     trace_media(P, s.o, s.d, s.time, 0.001f, id.gpix, id.sample0 + s.j, s.k, best);
   }
@@ -99,7 +99,7 @@ __global__ __launch_bounds__(256) void k_extend(Params P, int it) {
     Path s;
     load_path(P, slot, s);
     TravProf tp{};
-    const Hit best = intersect<LDS>(P, lnodes, recs_lds, ts, s, tp);
+    const Hit best = intersect<LDS, FT_ALL>(P, lnodes, recs_lds, ts, s, tp);
     P.hit[slot] = {best.t, best.u, best.v, bitsf(best.ref)};
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&P.ctr->segments, (unsigned long long)n);
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(256) void k_shade(Params P, int it) {
     const F4 hv = P.hit[slot];
     const Hit h = {hv.x, hv.y, hv.z, fbits(hv.w)};
     const WStack ws = {nullptr, 0};  // the weight stack outlives the launch: HBM only
-    int out = shade_core<true>(P, slot, s, h, ws);
+    int out = shade_core<true, FT_ALL>(P, slot, s, h, ws);
     if (out == OUT_NEED_CHUNK) {
       // static work split: slot s renders chunks s, s+P, s+2P, ... (no atomics)
       const uint32_t c = s.chunk + P.P;
@@ -171,8 +171,11 @@ __global__ __launch_bounds__(256) void k_init(Params P) {
 }
 
 // ----------------------------------------------------------------- fused ---
-template <bool LDS, int WAVES>
-__global__ __launch_bounds__(256, WAVES) void k_fused(Params P) {
+// 3 waves per SIMD (<= 170 VGPRs, 52 KB LDS per workgroup); FT = compiled-in
+// scene features (rt_device.h), chosen per scene by pick_fused
+constexpr int kFusedWaves = 3;
+template <bool LDS, uint32_t FT>
+__global__ __launch_bounds__(256, kFusedWaves) void k_fused(Params P) {
   __shared__ F4 lnodes[LDS ? 4 * kLdsNodes : 4];
   __shared__ uint32_t lstack[kShortStack * 256];
   __shared__ F4 lw[kLdsW * 256];
@@ -208,7 +211,7 @@ __global__ __launch_bounds__(256, WAVES) void k_fused(Params P) {
     RT_PHASE(0);
     if (has) {
       TravProf tp{};
-      const Hit best = intersect<LDS>(P, lnodes, recs_lds, ts, s, tp);
+      const Hit best = intersect<LDS, FT>(P, lnodes, recs_lds, ts, s, tp);
 #ifdef RT_PHASE_CLOCKS
       RT_PHASE(1);
       const unsigned long long act = __ballot(1);
@@ -227,7 +230,7 @@ __global__ __launch_bounds__(256, WAVES) void k_fused(Params P) {
       ck = clock64();
 #endif
       ++s.segs;
-      if (shade_core<false>(P, slot, s, best, ws) == OUT_NEED_CHUNK) has = false;
+      if (shade_core<false, FT>(P, slot, s, best, ws) == OUT_NEED_CHUNK) has = false;
     }
     RT_PHASE(2);
   }
@@ -483,21 +486,34 @@ static int occupancy_blocks(const void* kernel, int device, int* out) {
   return RT_OK;
 }
 
-// fused-kernel register budget (waves per SIMD); RT_FUSED_WAVES overrides (A/B tests)
-static int fused_waves() {
-  const char* e = getenv("RT_FUSED_WAVES");
-  int w = e ? atoi(e) : 3;
-  return (w == 3 || w == 4) ? w : 2;
-}
-static const void* pick_fused(bool lds, int waves) {
-  if (lds) {
-    if (waves == 4) return (const void*)k_fused<true, 4>;
-    if (waves == 3) return (const void*)k_fused<true, 3>;
-    return (const void*)k_fused<true, 2>;
+// Feature sets with a compiled fused kernel, smallest first; a scene runs the
+// first set that covers its features (scene_features).
+static constexpr uint32_t kFtSets[] = {
+    0u,                                                     // Cornell box: quads, Lambertian, light
+    FT_MEDIA,                                               // + constant media (Cornell smoke)
+    FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER,   // meshes and spheres, plain materials
+    FT_ALL};
+static_assert(FT_SPHERE == RT_FT_SPHERE && FT_TRI == RT_FT_TRI && FT_METAL == RT_FT_METAL &&
+                  FT_DIEL == RT_FT_DIEL && FT_MEDIA == RT_FT_MEDIA && FT_CHECKER == RT_FT_CHECKER &&
+                  FT_IMAGE == RT_FT_IMAGE && FT_NOISE == RT_FT_NOISE,
+              "feature bits: rt_device.h and rt_abi.h disagree");
+
+template <bool LDS>
+static const void* fused_for(uint32_t set) {
+  switch (set) {
+    case kFtSets[0]: return (const void*)k_fused<LDS, kFtSets[0]>;
+    case kFtSets[1]: return (const void*)k_fused<LDS, kFtSets[1]>;
+    case kFtSets[2]: return (const void*)k_fused<LDS, kFtSets[2]>;
+    default: return (const void*)k_fused<LDS, FT_ALL>;
   }
-  if (waves == 4) return (const void*)k_fused<false, 4>;
-  if (waves == 3) return (const void*)k_fused<false, 3>;
-  return (const void*)k_fused<false, 2>;
+}
+static uint32_t pick_set(uint32_t feats) {
+  for (uint32_t m : kFtSets)
+    if ((feats & ~m) == 0u) return m;
+  return FT_ALL;
+}
+static const void* pick_fused(bool lds, uint32_t set) {
+  return lds ? fused_for<true>(set) : fused_for<false>(set);
 }
 
 static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_opts* opts,
@@ -537,7 +553,8 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   uint32_t P;
   int fused_blocks = 0;
   const bool lds_nodes = s->h.nodes.size() / 4 <= (size_t)kLdsNodes;
-  const void* fused_kernel = pick_fused(lds_nodes, fused_waves());
+  const uint32_t feats = scene_features(s->h), ft_set = pick_set(feats);
+  const void* fused_kernel = pick_fused(lds_nodes, ft_set);
   if (mode == RT_MODE_FUSED) {
     if ((rc = occupancy_blocks(fused_kernel, o.device, &fused_blocks))) return rc;
     if (o.path_slots > 0) fused_blocks = std::max(1, std::min(fused_blocks, (o.path_slots + 255) / 256));
@@ -744,6 +761,8 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     stats->rows = (int32_t)rows;
     stats->mode = mode;
     stats->path_slots = (int32_t)P;
+    stats->kernel_features = mode == RT_MODE_FUSED ? (int32_t)ft_set : (int32_t)FT_ALL;
+    stats->scene_features = (int32_t)feats;
     auto sum_ms = [&](const std::vector<std::pair<int, int>>& v, double* acc) -> int {
       for (auto& pr : v) {
         float ms = 0;

@@ -230,7 +230,15 @@ typedef struct {
   int32_t n_materials, n_textures, n_images, n_perlins;
   int32_t medium_draws; /* total free-flight draws per vertex */
   int64_t device_bytes; /* scene bytes uploaded to HBM */
+  int32_t features;     /* RT_FT_* bits the scene needs (selects the fused kernel) */
+  int32_t _pad;
 } rt_scene_info;
+
+/* scene features (rt_scene_info.features, rt_stats.kernel_features) */
+enum {
+  RT_FT_SPHERE = 1, RT_FT_TRI = 2, RT_FT_METAL = 4, RT_FT_DIEL = 8, RT_FT_MEDIA = 16,
+  RT_FT_CHECKER = 32, RT_FT_IMAGE = 64, RT_FT_NOISE = 128
+};
 int rt_scene_info_get(const rt_scene* s, rt_scene_info* out);
 
 /* BVH export for structural tests: nodes as 16 floats
@@ -286,6 +294,8 @@ typedef struct {
   int32_t mode;          /* RT_MODE_* actually used */
   int32_t path_slots;    /* concurrent paths (wavefront slots / fused lanes) */
   double ms_fused;       /* fused-kernel time (RT_FLAG_PROFILE) */
+  int32_t kernel_features; /* RT_FT_* set compiled into the fused kernel that ran */
+  int32_t scene_features;  /* RT_FT_* set the scene needs */
 } rt_stats;
 
 /* Render this rank's rows; out_rgb (host) receives linear mean RGB
