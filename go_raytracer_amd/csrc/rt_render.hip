@@ -171,12 +171,13 @@ __global__ __launch_bounds__(256) void k_init(Params P) {
 }
 
 // ----------------------------------------------------------------- fused ---
-// 3 waves per SIMD (<= 170 VGPRs, 52 KB LDS per workgroup); FT = compiled-in
-// scene features (rt_device.h), chosen per scene by pick_fused
-constexpr int kFusedWaves = 3;
+// FT = compiled-in scene features (rt_device.h), chosen per scene by pick_fused.
+// Waves per SIMD by feature set: the lean sets fit more waves in the register
+// file (VGPRs <= 512 / waves) and in LDS (28 KB static + the scene cache).
+constexpr int fused_waves(uint32_t ft) { return ft == 0u ? 5 : ft == FT_MEDIA ? 4 : 3; }
 template <bool LDS, uint32_t FT>
-__global__ __launch_bounds__(256, kFusedWaves) void k_fused(Params P) {
-  __shared__ F4 lnodes[LDS ? 4 * kLdsNodes : 4];
+__global__ __launch_bounds__(256, fused_waves(FT)) void k_fused(Params P) {
+  extern __shared__ F4 lnodes[];  // LDS scene cache, sized at launch (scene_lds_bytes)
   __shared__ uint32_t lstack[kShortStack * 256];
   __shared__ F4 lw[kLdsW * 256];
   const bool recs_lds = LDS && stage_nodes(P, lnodes);
@@ -478,9 +479,9 @@ static int ensure_state(Scene* s, int device, uint32_t P, int depth_cap, uint32_
   return RT_OK;
 }
 
-static int occupancy_blocks(const void* kernel, int device, int* out) {
+static int occupancy_blocks(const void* kernel, int device, int* out, size_t dyn_lds = 0) {
   int per_cu = 0, cus = 0;
-  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0));
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, dyn_lds));
   HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
   *out = std::max(1, per_cu) * std::max(1, cus);
   return RT_OK;
@@ -555,8 +556,12 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   const bool lds_nodes = s->h.nodes.size() / 4 <= (size_t)kLdsNodes;
   const uint32_t feats = scene_features(s->h), ft_set = pick_set(feats);
   const void* fused_kernel = pick_fused(lds_nodes, ft_set);
+  // the fused kernel's LDS scene cache: nodes, then leaf records if both fit (stage_nodes)
+  const size_t n_nodes = s->h.nodes.size() / 4, n_refs = s->h.refs.size();
+  const size_t fused_lds =
+      lds_nodes ? 64 * (n_nodes + (n_nodes + n_refs <= (size_t)kLdsNodes ? n_refs : 0)) : 0;
   if (mode == RT_MODE_FUSED) {
-    if ((rc = occupancy_blocks(fused_kernel, o.device, &fused_blocks))) return rc;
+    if ((rc = occupancy_blocks(fused_kernel, o.device, &fused_blocks, fused_lds))) return rc;
     if (o.path_slots > 0) fused_blocks = std::max(1, std::min(fused_blocks, (o.path_slots + 255) / 256));
     P = (uint32_t)fused_blocks * 256u;
   } else {
@@ -675,7 +680,7 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
       HIP_OK(hipEventRecord(e0, stream));
     }
     void* args[] = {&p};
-    HIP_OK(hipLaunchKernel(fused_kernel, dim3(fused_blocks), dim3(256), args, 0, stream));
+    HIP_OK(hipLaunchKernel(fused_kernel, dim3(fused_blocks), dim3(256), args, fused_lds, stream));
     HIP_OK(hipGetLastError());
     if (prof) {
       HIP_OK(hipEventRecord(e1, stream));
