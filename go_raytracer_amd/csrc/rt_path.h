@@ -24,7 +24,6 @@ struct Counters {
   unsigned long long pushes;
   uint32_t chunk_head;
   uint32_t _pad[13];
-  unsigned long long prof[16];  // RT_PHASE_CLOCKS instrumentation
   uint32_t cnt[kMaxIt][kXcd];  // per-XCD queue lengths entering iteration i
 };
 
@@ -53,6 +52,8 @@ struct Params {
   uint32_t n_chunks;
   uint32_t P;          // path slots (stack column count)
   uint32_t ss;         // s*s
+  int step_budget;     // fused: traversal steps per scheduling round
+  uint32_t shade_min;  // fused: lanes that must be waiting before a wave shades
   uint64_t seed;
   // wavefront state (SoA, slot-indexed)
   F4* ray_o;   // origin | time
@@ -182,34 +183,41 @@ struct TravStack {
   }
 };
 
-#ifdef RT_PHASE_CLOCKS
-struct TravProf {
-  uint32_t inner, leaf, prims;
+// Resumable closest-hit traversal (replaces BVHNode.Hit bvh.go:69-82 +
+// HittableList.Hit hittable.go:122-138 + AABB.Hit aabb.go:90-113).  One step =
+// one inner node or one leaf; the fused kernel runs a bounded number of steps
+// per scheduling round so a lane that finishes early does not idle until the
+// wave's slowest ray is done (see k_fused).
+constexpr uint32_t TRAV_DONE = 0xFFFFFFFFu;  // never a node or leaf code (host_bvh.cpp)
+struct Trav {
+  f3 inv;
+  uint32_t cur;
+  int sp;
+  Hit best;
 };
-#define RT_TPROF(x) (x)
-#else
-struct TravProf {};
-#define RT_TPROF(x)
-#endif
+RT_D void trav_init(const DevScene& sc, f3 d, Trav& tr) {
+  tr.inv = mk3(rcp(d.x), rcp(d.y), rcp(d.z));
+  tr.cur = sc.root == PRIM_NONE ? TRAV_DONE : sc.root;
+  tr.sp = 0;
+  tr.best = {kInf, 0.0f, 0.0f, PRIM_NONE};
+}
 
 // LDS instantiation: lnodes holds the node array and, when recs_lds, the leaf
 // records right after it (uniform flag: both load forms exist, one runs)
 template <bool LDS, uint32_t FT>
-RT_D void trace_world(const DevScene& sc, const F4* lnodes, bool recs_lds, const TravStack& stack,
-                      f3 o, f3 d, float time, float tmin, Hit& best, TravProf& tp) {
-  if (sc.root == PRIM_NONE) return;
-  f3 inv = mk3(rcp(d.x), rcp(d.y), rcp(d.z));
-  int sp = 0;
-  uint32_t cur = sc.root;
-  for (;;) {
+RT_D void trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const TravStack& stack,
+                     f3 o, f3 d, float time, float tmin, Trav& tr, int budget) {
+  uint32_t cur = tr.cur;
+  int sp = tr.sp;
+  const f3 inv = tr.inv;
+  for (int n = 0; n < budget && cur != TRAV_DONE; ++n) {
     if (!(cur & LEAF_BIT)) {
-      RT_TPROF(++tp.inner);
       const F4* g = LDS ? lnodes + 4 * cur : sc.nodes + 4 * (size_t)cur;
       const F4 a0 = g[0], a1 = g[1], b0 = g[2], b1 = g[3];
       bool h0, h1;
       float t0, t1;
-      slab(a0, a1, o, inv, tmin, best.t, h0, t0);
-      slab(b0, b1, o, inv, tmin, best.t, h1, t1);
+      slab(a0, a1, o, inv, tmin, tr.best.t, h0, t0);
+      slab(b0, b1, o, inv, tmin, tr.best.t, h1, t1);
       uint32_t c0 = fbits(a0.w), c1 = fbits(a1.w);
       if (h0 && h1) {
         uint32_t nearc = t0 <= t1 ? c0 : c1, farc = t0 <= t1 ? c1 : c0;
@@ -217,18 +225,12 @@ RT_D void trace_world(const DevScene& sc, const F4* lnodes, bool recs_lds, const
         cur = nearc;
         continue;
       }
-      if (h0) {
-        cur = c0;
-        continue;
-      }
-      if (h1) {
-        cur = c1;
+      if (h0 || h1) {
+        cur = h0 ? c0 : c1;
         continue;
       }
     } else {
       uint32_t first = (cur >> 4) & 0x7FFFFFFu, count = (cur & 15u) + 1u;
-      RT_TPROF(++tp.leaf);
-      RT_TPROF(tp.prims += count);
       // leaf records are contiguous: no ref indirection, all four loads issue at once
       for (uint32_t k = 0; k < count; ++k) {
         const uint32_t ri = 4 * (first + k);
@@ -242,17 +244,28 @@ RT_D void trace_world(const DevScene& sc, const F4* lnodes, bool recs_lds, const
         }
         float t, u, v;
         uint32_t ref;
-        if (hit_record<FT>(rec, o, d, time, tmin, best.t, t, u, v, ref)) {
-          best.t = t;
-          best.u = u;
-          best.v = v;
-          best.ref = ref;
+        if (hit_record<FT>(rec, o, d, time, tmin, tr.best.t, t, u, v, ref)) {
+          tr.best.t = t;
+          tr.best.u = u;
+          tr.best.v = v;
+          tr.best.ref = ref;
         }
       }
     }
-    if (sp == 0) break;
-    cur = stack.pop(--sp);
+    cur = sp == 0 ? TRAV_DONE : stack.pop(--sp);
   }
+  tr.cur = cur;
+  tr.sp = sp;
+}
+
+// the whole traversal at once (wavefront extend kernel)
+template <bool LDS, uint32_t FT>
+RT_D void trace_world(const DevScene& sc, const F4* lnodes, bool recs_lds, const TravStack& stack,
+                      f3 o, f3 d, float time, float tmin, Hit& best) {
+  Trav tr;
+  trav_init(sc, d, tr);
+  trav_steps<LDS, FT>(sc, lnodes, recs_lds, stack, o, d, time, tmin, tr, 0x7FFFFFFF);
+  best = tr.best;
 }
 
 // closest boundary hit over (lo, hi) with each prim's own interval semantics

@@ -52,18 +52,14 @@ RT_D void record_trace(const Params& P, const Path& s, const Hit& best) {
   }
 }
 
-// closest hit of one path (world BVH + media), camera.go:300
-template <bool LDS, uint32_t FT>
-RT_D Hit intersect(const Params& P, const F4* lnodes, bool recs_lds, const TravStack& ts,
-                   const Path& s, TravProf& tp) {
-  Hit best = {kInf, 0.0f, 0.0f, PRIM_NONE};
-  trace_world<LDS, FT>(P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, best, tp);
+// media + debug trace on top of the world closest hit, camera.go:300
+template <uint32_t FT>
+RT_D void finish_hit(const Params& P, const Path& s, Hit& best) {
   if (HAS(FT_MEDIA) && P.sc.n_media > 0) {
     const Ids id = chunk_ids(P, s.chunk);
     trace_media(P, s.o, s.d, s.time, 0.001f, id.gpix, id.sample0 + s.j, s.k, best);
   }
   if (P.trace) record_trace(P, s, best);
-  return best;
 }
 
 // ------------------------------------------------------------- wavefront ---
@@ -98,8 +94,9 @@ __global__ __launch_bounds__(256) void k_extend(Params P, int it) {
     const uint32_t slot = queue_slot(P, q, cnt, i);
     Path s;
     load_path(P, slot, s);
-    TravProf tp{};
-    const Hit best = intersect<LDS, FT_ALL>(P, lnodes, recs_lds, ts, s, tp);
+    Hit best;
+    trace_world<LDS, FT_ALL>(P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, best);
+    finish_hit<FT_ALL>(P, s, best);
     P.hit[slot] = {best.t, best.u, best.v, bitsf(best.ref)};
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&P.ctr->segments, (unsigned long long)n);
@@ -187,59 +184,37 @@ __global__ __launch_bounds__(256, fused_waves(FT)) void k_fused(Params P) {
   Path s;
   s.segs = 0;
   s.pushes = 0;
+  Trav tr;
+  tr.cur = TRAV_DONE;
   bool has = false;
   WaveBatch b = {0u, 0u};
-#ifdef RT_PHASE_CLOCKS
-  // per-wave phase clocks and SIMD-utilisation counters (profiling build only)
-  unsigned long long pc[16] = {};
-  unsigned long long tw0 = wall_clock64(), ck = clock64();
-#define RT_PHASE(i)                      \
-  do {                                   \
-    const unsigned long long n_ = clock64(); \
-    pc[i] += n_ - ck;                    \
-    ck = n_;                             \
-  } while (0)
-#else
-#define RT_PHASE(i)
-#endif
+  // Scheduling round: lanes without work take a chunk; traversing lanes run up
+  // to step_budget traversal steps; lanes whose traversal is done are shaded
+  // together once at least shade_min of them wait (or nothing else traverses),
+  // so traversal divergence costs idle lanes only until the next round.
   for (;;) {
     const uint32_t c = grab_chunk(P, b, !has);
     if (c != 0xFFFFFFFFu) {
       start_sample<false>(P, slot, s, c, 0);
+      trav_init(P.sc, s.d, tr);
       has = true;
     }
     if (!__any(has)) break;
-    RT_PHASE(0);
-    if (has) {
-      TravProf tp{};
-      const Hit best = intersect<LDS, FT>(P, lnodes, recs_lds, ts, s, tp);
-#ifdef RT_PHASE_CLOCKS
-      RT_PHASE(1);
-      const unsigned long long act = __ballot(1);
-      pc[3] += 1;
-      pc[4] += __popcll(act);
-      uint32_t mi = tp.inner, ml = tp.leaf, si = tp.inner, sl = tp.leaf, sp = tp.prims, mp = tp.prims;
-      for (int off = 32; off > 0; off >>= 1) {
-        mi = max(mi, (uint32_t)__shfl_xor((int)mi, off));
-        ml = max(ml, (uint32_t)__shfl_xor((int)ml, off));
-        mp = max(mp, (uint32_t)__shfl_xor((int)mp, off));
-        si += __shfl_xor(si, off);
-        sl += __shfl_xor(sl, off);
-        sp += __shfl_xor(sp, off);
+    if (has && tr.cur != TRAV_DONE)
+      trav_steps<LDS, FT>(P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, tr, P.step_budget);
+    const bool ready = has && tr.cur == TRAV_DONE;
+    const uint32_t n_ready = (uint32_t)__popcll(__ballot(ready));
+    const bool busy = __any(has && !ready);
+    if (n_ready >= P.shade_min || !busy) {
+      if (ready) {
+        Hit best = tr.best;
+        finish_hit<FT>(P, s, best);
+        ++s.segs;
+        if (shade_core<false, FT>(P, slot, s, best, ws) == OUT_NEED_CHUNK) has = false;
+        else trav_init(P.sc, s.d, tr);
       }
-      pc[5] += mi; pc[6] += si; pc[7] += ml; pc[8] += sl; pc[9] += mp; pc[10] += sp;
-      ck = clock64();
-#endif
-      ++s.segs;
-      if (shade_core<false, FT>(P, slot, s, best, ws) == OUT_NEED_CHUNK) has = false;
     }
-    RT_PHASE(2);
   }
-#ifdef RT_PHASE_CLOCKS
-  pc[11] = wall_clock64() - tw0;
-  if (lane_id() == 0)
-    for (int i = 0; i < 12; ++i) atomicAdd(&P.ctr->prof[i], pc[i]);
-#endif
   uint32_t segs = s.segs, pushes = s.pushes;
   for (int off = 32; off > 0; off >>= 1) {
     segs += __shfl_xor(segs, off);
@@ -335,6 +310,12 @@ static int upload(DeviceScene* ds, const std::vector<T>& v, const T** out) {
   HIP_OK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
   *out = (const T*)p;
   return RT_OK;
+}
+
+// scheduling knobs of the fused kernel (A/B experiments; defaults measured)
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e && *e ? atoi(e) : dflt;
 }
 
 static FastDiv make_fastdiv(uint32_t d) {
@@ -625,6 +606,10 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   p.fd_npix = make_fastdiv(npix);
   p.fd_width = make_fastdiv(W);
   p.fd_s = make_fastdiv((uint32_t)cd.spp_sqrt);
+  // measured (tools/sched_sweep.py): an unbounded budget is best on every demo
+  // scene, i.e. traversal divergence is not what limits the fused kernel
+  p.step_budget = env_int("RT_STEP_BUDGET", 1 << 30);
+  p.shade_min = (uint32_t)env_int("RT_SHADE_MIN", 1);
   p.seed = o.seed;
   p.ray_o = st->ray_o;
   p.ray_d = st->ray_d;
@@ -748,13 +733,6 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     Counters hc;
     HIP_OK(hipMemcpy(&hc, st->ctr, offsetof(Counters, cnt), hipMemcpyDeviceToHost));
     stats->samples = (uint64_t)npix * ss;
-#ifdef RT_PHASE_CLOCKS
-    fprintf(stderr,
-            "[rt phase] grab %llu isect %llu shade %llu | iters %llu active_lanes %llu | "
-            "inner max %llu sum %llu | leaf max %llu sum %llu | prims max %llu sum %llu | wall %llu\n",
-            hc.prof[0], hc.prof[1], hc.prof[2], hc.prof[3], hc.prof[4], hc.prof[5], hc.prof[6],
-            hc.prof[7], hc.prof[8], hc.prof[9], hc.prof[10], hc.prof[11]);
-#endif
     stats->segments = hc.segments;
     stats->stack_pushes = hc.pushes;
     stats->extend_rays = hc.segments;

@@ -1,4 +1,5 @@
-"""Quick GPU timing probe: render a config once and print throughput (dev tool)."""
+"""Quick GPU timing probe: render a config once and print throughput (dev tool).
+usage: gpu_probe.py scene width spp [modes] [aspect]"""
 import sys, time, json
 sys.path.insert(0, ".")
 import go_raytracer_amd as rt
@@ -6,15 +7,18 @@ import go_raytracer_amd as rt
 scene = sys.argv[1] if len(sys.argv) > 1 else "cornell"
 width = int(sys.argv[2]) if len(sys.argv) > 2 else 800
 spp = int(sys.argv[3]) if len(sys.argv) > 3 else 64
+modes = sys.argv[4].split(",") if len(sys.argv) > 4 else ["fused", "wavefront"]
 t, cam, w, l = rt.demo_scene(scene)
 cam.Width = width
-cam.SamplesPerPixel = spp
-if scene == "book1":
+if len(sys.argv) > 5:
+    cam.AspectRatio = float(sys.argv[5])
+elif scene == "book1":
     cam.AspectRatio = 1.5
-modes = sys.argv[4].split(",") if len(sys.argv) > 4 else ["fused", "wavefront"]
 with rt.Scene(t, w, l) as sc:
     for mode in modes:
-        img, st = sc.render(cam, seed=1, profile=True, mode=mode)  # warm (upload)
+        cam.SamplesPerPixel = 1
+        sc.render(cam, seed=1, mode=mode)  # warm: upload + state buffers
+        cam.SamplesPerPixel = spp
         t0 = time.time()
         img, st = sc.render(cam, seed=1, profile=True, mode=mode)
         dt = time.time() - t0
