@@ -54,6 +54,7 @@ struct Params {
   uint32_t ss;         // s*s
   int step_budget;     // fused: traversal steps per scheduling round
   uint32_t shade_min;  // fused: lanes that must be waiting before a wave shades
+  uint32_t recs_lds;   // leaf records cached in LDS after the nodes (stage_nodes)
   uint64_t seed;
   // wavefront state (SoA, slot-indexed)
   F4* ray_o;   // origin | time

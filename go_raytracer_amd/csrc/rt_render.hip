@@ -35,7 +35,7 @@ namespace rt {
 RT_D bool stage_nodes(const Params& P, F4* lnodes) {
   const int nl = min(P.sc.n_nodes, kLdsNodes);
   for (int i = threadIdx.x; i < 4 * nl; i += blockDim.x) lnodes[i] = P.sc.nodes[i];
-  const bool recs = P.sc.n_nodes + P.sc.n_refs <= kLdsNodes;
+  const bool recs = P.recs_lds != 0u;
   if (recs)
     for (int i = threadIdx.x; i < 4 * P.sc.n_refs; i += blockDim.x)
       lnodes[4 * nl + i] = P.sc.leafprims[i];
@@ -536,11 +536,17 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   int fused_blocks = 0;
   const bool lds_nodes = s->h.nodes.size() / 4 <= (size_t)kLdsNodes;
   const uint32_t feats = scene_features(s->h), ft_set = pick_set(feats);
-  const void* fused_kernel = pick_fused(lds_nodes, ft_set);
-  // the fused kernel's LDS scene cache: nodes, then leaf records if both fit (stage_nodes)
+  // The fused kernel's LDS scene cache (stage_nodes): all BVH nodes, then the
+  // leaf records when both fit, within the LDS a workgroup may take at the
+  // kernel's target waves per SIMD (160 KB per CU, 28 KB of stacks per group).
+  // A tree that does not fit runs the global-node instantiation: caching only
+  // its top measured 3-6 % slower on C3-C5 than one node source per kernel.
   const size_t n_nodes = s->h.nodes.size() / 4, n_refs = s->h.refs.size();
-  const size_t fused_lds =
-      lds_nodes ? 64 * (n_nodes + (n_nodes + n_refs <= (size_t)kLdsNodes ? n_refs : 0)) : 0;
+  const size_t lds_slots = std::min<size_t>(
+      kLdsNodes, (160u * 1024u / (unsigned)fused_waves(ft_set) - 28u * 1024u - 512u) / 64u);
+  const bool f_lds = n_nodes <= lds_slots;
+  const void* fused_kernel = pick_fused(f_lds, ft_set);
+  const size_t fused_lds = f_lds ? 64 * (n_nodes + (n_nodes + n_refs <= lds_slots ? n_refs : 0)) : 0;
   if (mode == RT_MODE_FUSED) {
     if ((rc = occupancy_blocks(fused_kernel, o.device, &fused_blocks, fused_lds))) return rc;
     if (o.path_slots > 0) fused_blocks = std::max(1, std::min(fused_blocks, (o.path_slots + 255) / 256));
@@ -609,6 +615,7 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   // measured (tools/sched_sweep.py): an unbounded budget is best on every demo
   // scene, i.e. traversal divergence is not what limits the fused kernel
   p.step_budget = env_int("RT_STEP_BUDGET", 1 << 30);
+  p.recs_lds = f_lds && n_nodes + n_refs <= lds_slots ? 1u : 0u;
   p.shade_min = (uint32_t)env_int("RT_SHADE_MIN", 1);
   p.seed = o.seed;
   p.ray_o = st->ray_o;
