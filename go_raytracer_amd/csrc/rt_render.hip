@@ -612,11 +612,12 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   p.fd_npix = make_fastdiv(npix);
   p.fd_width = make_fastdiv(W);
   p.fd_s = make_fastdiv((uint32_t)cd.spp_sqrt);
-  // measured (tools/sched_sweep.py): an unbounded budget is best on every demo
-  // scene, i.e. traversal divergence is not what limits the fused kernel
-  p.step_budget = env_int("RT_STEP_BUDGET", 1 << 30);
-  p.recs_lds = f_lds && n_nodes + n_refs <= lds_slots ? 1u : 0u;
+  // Measured on the full-size configs (tools/sched_sweep.py, profiles/): deep
+  // trees (C5, 1M triangles) gain ~45 % from bounded rounds of 8-12 steps with
+  // shading every round; shallow trees (C2, C3) lose 3-30 % from any bound.
+  p.step_budget = env_int("RT_STEP_BUDGET", n_nodes > 16384 ? 10 : (1 << 30));
   p.shade_min = (uint32_t)env_int("RT_SHADE_MIN", 1);
+  p.recs_lds = f_lds && n_nodes + n_refs <= lds_slots ? 1u : 0u;
   p.seed = o.seed;
   p.ray_o = st->ray_o;
   p.ray_d = st->ray_d;
