@@ -5,6 +5,7 @@
 // visits both children of every node, left first (bvh.go:21-82).  The closest
 // hit does not depend on the topology (ties aside), so the device tree is our
 // own: SAH splits, leaves of up to 4 prims, near-child-first traversal.
+#include <stdlib.h>
 #include <math.h>
 #include <string.h>
 
@@ -46,14 +47,27 @@ struct TmpNode {
 };
 
 constexpr int kBins = 16;
-constexpr int kLeafTarget = 4;  // SAH may stop at <= 4 prims
-constexpr double kCostTrav = 1.0, kCostIsect = 1.0;
+// SAH leaf/split trade-off; RT_BVH_LEAF / RT_BVH_CT / RT_BVH_CI override (tuning)
+static int env_i(const char* n, int d) {
+  const char* e = getenv(n);
+  return e && *e ? atoi(e) : d;
+}
+static double env_d(const char* n, double d) {
+  const char* e = getenv(n);
+  return e && *e ? atof(e) : d;
+}
 
 }  // namespace
 
 int build_bvh(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi,
               const std::vector<uint32_t>& prims) {
   const int n = (int)prims.size();
+  // SAH may stop at <= kLeafTarget prims.  Measured (tools/bvh_sweep.sh, profiles/):
+  // small scenes, whose leaves sit in LDS, are fastest with leaves of up to 4;
+  // large ones (C4 3.4k prims, C5 1M) are 11 % faster with single-prim leaves,
+  // the parent's child box culling each prim before its record is fetched.
+  const int kLeafTarget = std::min(env_i("RT_BVH_LEAF", n > 1024 ? 1 : 4), MAX_LEAF);
+  const double kCostTrav = env_d("RT_BVH_CT", 1.0), kCostIsect = env_d("RT_BVH_CI", 1.0);
   s.nodes.clear();
   s.refs.clear();
   s.prim_bounds.clear();
