@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 #include <deque>
 
 #include "rt_internal.h"
@@ -216,7 +217,8 @@ int build_bvh(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi
       return set_error(RT_ERR_UNSUPPORTED, "BVH leaf of %d prims exceeds %d", x.count, MAX_LEAF);
 
   if (tn[0].left < 0) {
-    s.root = leaf_of(tn[0]);
+    s.root = s.root4 = leaf_of(tn[0]);
+    s.nodes4.clear();
     return RT_OK;
   }
   // BFS numbering of inner nodes
@@ -249,6 +251,62 @@ int build_bvh(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi
     s.nodes[4 * o + 3] = {b.box.mx[0], b.box.mx[1], b.box.mx[2], 0};
   }
   s.root = 0;
+
+  // BVH4 by collapsing the binary tree: a BVH4 node starts from a BVH2 inner
+  // node's two children and keeps replacing its largest-area inner child by
+  // that child's two children until it has four or only leaves are left.
+  // Leaves (and so the leaf records) are shared with the BVH2.
+  std::vector<std::array<int, 4>> kids;
+  std::vector<int> nkids;
+  std::deque<int> q4 = {0};
+  std::vector<int> out4(tn.size(), -1);
+  std::vector<int> order4;
+  while (!q4.empty()) {
+    int i = q4.front();
+    q4.pop_front();
+    out4[i] = (int)order4.size();
+    order4.push_back(i);
+    std::array<int, 4> ch = {tn[i].left, tn[i].right, -1, -1};
+    int nc = 2;
+    while (nc < 4) {
+      int best = -1;
+      double best_area = -1;
+      for (int k = 0; k < nc; ++k)
+        if (tn[ch[k]].left >= 0 && tn[ch[k]].box.area() > best_area) {
+          best_area = tn[ch[k]].box.area();
+          best = k;
+        }
+      if (best < 0) break;
+      const int c = ch[best];
+      ch[best] = tn[c].left;
+      ch[nc++] = tn[c].right;
+    }
+    for (int k = 0; k < nc; ++k)
+      if (tn[ch[k]].left >= 0) q4.push_back(ch[k]);
+    kids.push_back(ch);
+    nkids.push_back(nc);
+  }
+  s.nodes4.assign(8 * order4.size(), F4{0, 0, 0, 0});
+  for (size_t o = 0; o < order4.size(); ++o) {
+    F4* nd = &s.nodes4[8 * o];
+    float* lx = &nd[0].x;  // the 8 F4 as 32 floats: [field][child]
+    for (int k = 0; k < 4; ++k) {
+      uint32_t code = CHILD_EMPTY;
+      Box b;  // empty slot: a point box at the origin, skipped by its code
+      for (int a = 0; a < 3; ++a) b.mn[a] = b.mx[a] = 0.0f;
+      if (k < nkids[o]) {
+        const TmpNode& c = tn[kids[o][k]];
+        b = c.box;
+        code = c.left >= 0 ? (uint32_t)out4[kids[o][k]] : leaf_of(c);
+      }
+      for (int a = 0; a < 3; ++a) {
+        lx[(2 * a) * 4 + k] = b.mn[a];
+        lx[(2 * a + 1) * 4 + k] = b.mx[a];
+      }
+      lx[6 * 4 + k] = bits(code);
+    }
+  }
+  s.root4 = 0;
   return RT_OK;
 }
 

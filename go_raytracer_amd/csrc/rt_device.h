@@ -34,6 +34,12 @@ inline constexpr uint32_t leaf_code(uint32_t first, uint32_t count) {
   return LEAF_BIT | (first << 4) | (count - 1u);
 }
 
+// ---- BVH4 node: four children's boxes in the parent, SoA (128 B) -----------
+//  f4[0] = lo.x of children 0..3   f4[1] = hi.x   f4[2] = lo.y   f4[3] = hi.y
+//  f4[4] = lo.z                   f4[5] = hi.z   f4[6] = child codes (bits)  f4[7] = 0
+// child code: inner BVH4 node index, leaf code (LEAF_BIT, as BVH2), or CHILD_EMPTY
+constexpr uint32_t CHILD_EMPTY = 0xFFFFFFFEu;
+
 // ---- per-type primitive records ------------------------------------------
 // sphere (objects.go:14-37): sph_cr = center@t0 | radius ; sph_mv = motion | mat bits
 //   sph_uv = cos,sin of the baked Y rotation (UV is computed in object space, objects.go:113)

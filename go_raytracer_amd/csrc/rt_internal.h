@@ -43,7 +43,9 @@ struct HostScene {
   std::vector<F4> quad;      // 5 per quad
   std::vector<F4> tri;       // 3 per tri
   std::vector<F4> tri_attr;  // 6 per tri
-  std::vector<F4> nodes;     // 4 per node
+  std::vector<F4> nodes;     // BVH2, 4 per node (export / structural tests)
+  std::vector<F4> nodes4;    // BVH4 the kernels traverse, 8 per node (rt_device.h)
+  uint32_t root4 = PRIM_NONE;
   std::vector<uint32_t> refs;
   uint32_t root = PRIM_NONE;
   std::vector<float> prim_bounds;  // 6 per world ref (export/tests)

@@ -30,15 +30,15 @@
 
 namespace rt {
 
-// the whole BVH node array -> LDS (only used when n_nodes <= kLdsNodes), then
-// the leaf records when they fit too; returns whether they did
+// the whole BVH4 node array -> LDS (only used when 2 * n_nodes <= kLdsNodes
+// 64-B slots), then the leaf records when they fit too; returns whether they did
 RT_D bool stage_nodes(const Params& P, F4* lnodes) {
-  const int nl = min(P.sc.n_nodes, kLdsNodes);
-  for (int i = threadIdx.x; i < 4 * nl; i += blockDim.x) lnodes[i] = P.sc.nodes[i];
+  const int nl = min(P.sc.n_nodes, kLdsNodes / 2);
+  for (int i = threadIdx.x; i < 8 * nl; i += blockDim.x) lnodes[i] = P.sc.nodes[i];
   const bool recs = P.recs_lds != 0u;
   if (recs)
     for (int i = threadIdx.x; i < 4 * P.sc.n_refs; i += blockDim.x)
-      lnodes[4 * nl + i] = P.sc.leafprims[i];
+      lnodes[8 * nl + i] = P.sc.leafprims[i];
   __syncthreads();
   return recs;
 }
@@ -396,7 +396,7 @@ static int ensure_scene(Scene* s, int device) {
   UP(h.quad, quad);
   UP(h.tri, tri);
   UP(h.tri_attr, tri_attr);
-  UP(h.nodes, nodes);
+  UP(h.nodes4, nodes);
   UP(h.refs, refs);
   {
     std::vector<F4> recs;
@@ -412,8 +412,8 @@ static int ensure_scene(Scene* s, int device) {
   UP(h.images, images);
   UP(h.perlins, perlins);
 #undef UP
-  d.root = h.root;
-  d.n_nodes = (int32_t)(h.nodes.size() / 4);
+  d.root = h.root4;
+  d.n_nodes = (int32_t)(h.nodes4.size() / 8);
   d.n_media = (int32_t)h.media.size();
   d.medium_draws = h.medium_draws;
   d.n_lights = (int32_t)h.lights.size();
@@ -534,19 +534,20 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   const int depth_cap = cd.max_depth + 1;
   uint32_t P;
   int fused_blocks = 0;
-  const bool lds_nodes = s->h.nodes.size() / 4 <= (size_t)kLdsNodes;
+  const bool lds_nodes = s->h.nodes4.size() / 8 <= (size_t)kLdsNodes / 2;
   const uint32_t feats = scene_features(s->h), ft_set = pick_set(feats);
   // The fused kernel's LDS scene cache (stage_nodes): all BVH nodes, then the
   // leaf records when both fit, within the LDS a workgroup may take at the
   // kernel's target waves per SIMD (160 KB per CU, 28 KB of stacks per group).
   // A tree that does not fit runs the global-node instantiation: caching only
   // its top measured 3-6 % slower on C3-C5 than one node source per kernel.
-  const size_t n_nodes = s->h.nodes.size() / 4, n_refs = s->h.refs.size();
+  const size_t n_nodes = s->h.nodes4.size() / 8, n_refs = s->h.refs.size();  // BVH4
   const size_t lds_slots = std::min<size_t>(
       kLdsNodes, (160u * 1024u / (unsigned)fused_waves(ft_set) - 28u * 1024u - 512u) / 64u);
-  const bool f_lds = n_nodes <= lds_slots;
+  const bool f_lds = 2 * n_nodes <= lds_slots;
   const void* fused_kernel = pick_fused(f_lds, ft_set);
-  const size_t fused_lds = f_lds ? 64 * (n_nodes + (n_nodes + n_refs <= lds_slots ? n_refs : 0)) : 0;
+  const size_t fused_lds =
+      f_lds ? 64 * (2 * n_nodes + (2 * n_nodes + n_refs <= lds_slots ? n_refs : 0)) : 0;
   if (mode == RT_MODE_FUSED) {
     if ((rc = occupancy_blocks(fused_kernel, o.device, &fused_blocks, fused_lds))) return rc;
     if (o.path_slots > 0) fused_blocks = std::max(1, std::min(fused_blocks, (o.path_slots + 255) / 256));
@@ -615,9 +616,9 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   // Measured on the full-size configs (tools/sched_sweep.py, profiles/): deep
   // trees (C5, 1M triangles) gain ~45 % from bounded rounds of 8-12 steps with
   // shading every round; shallow trees (C2, C3) lose 3-30 % from any bound.
-  p.step_budget = env_int("RT_STEP_BUDGET", n_nodes > 16384 ? 10 : (1 << 30));
+  p.step_budget = env_int("RT_STEP_BUDGET", n_nodes > 6000 ? 6 : (1 << 30));
   p.shade_min = (uint32_t)env_int("RT_SHADE_MIN", 1);
-  p.recs_lds = f_lds && n_nodes + n_refs <= lds_slots ? 1u : 0u;
+  p.recs_lds = f_lds && 2 * n_nodes + n_refs <= lds_slots ? 1u : 0u;
   p.seed = o.seed;
   p.ray_o = st->ray_o;
   p.ray_d = st->ray_d;
