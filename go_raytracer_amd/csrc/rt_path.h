@@ -158,6 +158,7 @@ typedef __attribute__((address_space(1))) uint32_t glb_u32;
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4f lds_v4;
 typedef __attribute__((address_space(1))) v4f glb_v4;
+typedef float v2f __attribute__((ext_vector_type(2)));
 RT_D F4 ld_lds(const F4* p) {
   const v4f v = *(const lds_v4*)p;
   return {v.x, v.y, v.z, v.w};
@@ -167,6 +168,11 @@ RT_D F4 ld_glb(const F4* p) {
   return {v.x, v.y, v.z, v.w};
 }
 RT_D void st_lds(F4* p, F4 v) { *(lds_v4*)p = v4f{v.x, v.y, v.z, v.w}; }
+// s_waitcnt vmcnt(0) (gfx9 encoding: expcnt/lgkmcnt left unconstrained).  Placed
+// at the end of a RARE global-memory branch whose result merges with an LDS
+// branch: without it the compiler's wait lands after the merge, on the common
+// LDS path too, where it drains every outstanding store and atomic.
+RT_D void wait_vm() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 RT_D void st_glb(F4* p, F4 v) { *(glb_v4*)p = v4f{v.x, v.y, v.z, v.w}; }
 struct TravStack {
   uint32_t* lds;     // &lds_stack[0][threadIdx.x], stride blockDim.x
@@ -178,8 +184,12 @@ struct TravStack {
   }
   RT_D uint32_t pop(int sp) const {
     uint32_t v;
-    if (sp < kShortStack) v = ((lds_u32*)lds)[sp * 256];
-    else v = ((glb_u32*)ovf)[(size_t)(sp - kShortStack) * cols];
+    if (sp < kShortStack) {
+      v = ((lds_u32*)lds)[sp * 256];
+    } else {
+      v = ((glb_u32*)ovf)[(size_t)(sp - kShortStack) * cols];
+      wait_vm();
+    }
     return v;
   }
 };
@@ -213,21 +223,48 @@ RT_D void trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const 
   const f3 inv = tr.inv;
   for (int n = 0; n < budget && cur != TRAV_DONE; ++n) {
     if (!(cur & LEAF_BIT)) {
-      const F4* g = LDS ? lnodes + 4 * cur : sc.nodes + 4 * (size_t)cur;
-      const F4 a0 = g[0], a1 = g[1], b0 = g[2], b1 = g[3];
-      bool h0, h1;
-      float t0, t1;
-      slab(a0, a1, o, inv, tmin, tr.best.t, h0, t0);
-      slab(b0, b1, o, inv, tmin, tr.best.t, h1, t1);
-      uint32_t c0 = fbits(a0.w), c1 = fbits(a1.w);
-      if (h0 && h1) {
-        uint32_t nearc = t0 <= t1 ? c0 : c1, farc = t0 <= t1 ? c1 : c0;
-        if (sp < kStack) stack.push(sp++, farc);
-        cur = nearc;
-        continue;
+      // BVH4 node: four slab tests, children ordered front to back; the
+      // nearest is visited next, the others pushed farthest first
+      const F4* g = LDS ? lnodes + 8 * cur : sc.nodes + 8 * (size_t)cur;
+      const F4 lx = g[0], hx = g[1], ly = g[2], hy = g[3], lz = g[4], hz = g[5], cc = g[6];
+      const float tmax = tr.best.t;
+      float tn[4];
+      uint32_t ch[4];
+      const float Lx[4] = {lx.x, lx.y, lx.z, lx.w}, Hx[4] = {hx.x, hx.y, hx.z, hx.w};
+      const float Ly[4] = {ly.x, ly.y, ly.z, ly.w}, Hy[4] = {hy.x, hy.y, hy.z, hy.w};
+      const float Lz[4] = {lz.x, lz.y, lz.z, lz.w}, Hz[4] = {hz.x, hz.y, hz.z, hz.w};
+      const uint32_t C[4] = {fbits(cc.x), fbits(cc.y), fbits(cc.z), fbits(cc.w)};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float tx0 = (Lx[k] - o.x) * inv.x, tx1 = (Hx[k] - o.x) * inv.x;
+        const float ty0 = (Ly[k] - o.y) * inv.y, ty1 = (Hy[k] - o.y) * inv.y;
+        const float tz0 = (Lz[k] - o.z) * inv.z, tz1 = (Hz[k] - o.z) * inv.z;
+        const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
+        const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+        const bool h = t0 <= t1 * 1.00000024f && C[k] != CHILD_EMPTY;  // slab() semantics
+        tn[k] = h ? t0 : kInf;
+        ch[k] = C[k];
       }
-      if (h0 || h1) {
-        cur = h0 ? c0 : c1;
+      // sorting network (0,1)(2,3)(0,2)(1,3)(1,2): ascending entry distance
+      auto cx = [&](int a, int b) {
+        const bool sw = tn[b] < tn[a];
+        const float ta = tn[a], tb = tn[b];
+        const uint32_t ca = ch[a], cb = ch[b];
+        tn[a] = sw ? tb : ta;
+        tn[b] = sw ? ta : tb;
+        ch[a] = sw ? cb : ca;
+        ch[b] = sw ? ca : cb;
+      };
+      cx(0, 1);
+      cx(2, 3);
+      cx(0, 2);
+      cx(1, 3);
+      cx(1, 2);
+      if (tn[0] != kInf) {
+        if (tn[3] != kInf && sp < kStack) stack.push(sp++, ch[3]);
+        if (tn[2] != kInf && sp < kStack) stack.push(sp++, ch[2]);
+        if (tn[1] != kInf && sp < kStack) stack.push(sp++, ch[1]);
+        cur = ch[0];
         continue;
       }
     } else {
@@ -237,11 +274,12 @@ RT_D void trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const 
         const uint32_t ri = 4 * (first + k);
         F4 rec[4];
         if (LDS && recs_lds) {
-          const F4* q = lnodes + 4 * sc.n_nodes + ri;
+          const F4* q = lnodes + 8 * sc.n_nodes + ri;
           for (int e = 0; e < 4; ++e) rec[e] = ld_lds(q + e);
         } else {
           const F4* q = sc.leafprims + ri;
           for (int e = 0; e < 4; ++e) rec[e] = ld_glb(q + e);
+          if (LDS) wait_vm();  // LDS kernel whose records did not fit: keep the wait here
         }
         float t, u, v;
         uint32_t ref;
@@ -558,8 +596,12 @@ struct WStack {
   }
   RT_D F4 get(const Params& P, uint32_t slot, uint32_t k) const {
     F4 v;
-    if ((int)k < nlds) v = ld_lds(lds + k * 256);
-    else v = ld_glb(P.stack + (size_t)(k - nlds) * P.P + slot);
+    if ((int)k < nlds) {
+      v = ld_lds(lds + k * 256);
+    } else {
+      v = ld_glb(P.stack + (size_t)(k - nlds) * P.P + slot);
+      if (nlds > 0) wait_vm();
+    }
     return v;
   }
 };
