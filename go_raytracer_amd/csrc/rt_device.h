@@ -111,7 +111,7 @@ struct DevScene {
   const F4* quad;
   const F4* tri;
   const F4* tri_attr;
-  const F4* nodes;
+  const F4* nodes;      // the tree this launch traverses (BVH4, or BVH2 for tiny scenes)
   const uint32_t* refs;
   const F4* leafprims;  // 4 x F4 per leaf entry, parallel to refs (see "leaf records")
   uint32_t root;

@@ -215,14 +215,33 @@ RT_D void trav_init(const DevScene& sc, f3 d, Trav& tr) {
 
 // LDS instantiation: lnodes holds the node array and, when recs_lds, the leaf
 // records right after it (uniform flag: both load forms exist, one runs)
-template <bool LDS, uint32_t FT>
+template <bool LDS, uint32_t FT, bool W4 = true>
 RT_D void trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const TravStack& stack,
                      f3 o, f3 d, float time, float tmin, Trav& tr, int budget) {
   uint32_t cur = tr.cur;
   int sp = tr.sp;
   const f3 inv = tr.inv;
   for (int n = 0; n < budget && cur != TRAV_DONE; ++n) {
-    if (!(cur & LEAF_BIT)) {
+    if (!W4 && !(cur & LEAF_BIT)) {
+      // BVH2 node (tiny scenes, see render_impl): both child boxes, nearer first
+      const F4* g = LDS ? lnodes + 4 * cur : sc.nodes + 4 * (size_t)cur;
+      const F4 a0 = g[0], a1 = g[1], b0 = g[2], b1 = g[3];
+      bool h0, h1;
+      float t0, t1;
+      slab(a0, a1, o, inv, tmin, tr.best.t, h0, t0);
+      slab(b0, b1, o, inv, tmin, tr.best.t, h1, t1);
+      const uint32_t c0 = fbits(a0.w), c1 = fbits(a1.w);
+      if (h0 && h1) {
+        const uint32_t nearc = t0 <= t1 ? c0 : c1, farc = t0 <= t1 ? c1 : c0;
+        if (sp < kStack) stack.push(sp++, farc);
+        cur = nearc;
+        continue;
+      }
+      if (h0 || h1) {
+        cur = h0 ? c0 : c1;
+        continue;
+      }
+    } else if (W4 && !(cur & LEAF_BIT)) {
       // BVH4 node: four slab tests, children ordered front to back; the
       // nearest is visited next, the others pushed farthest first
       const F4* g = LDS ? lnodes + 8 * cur : sc.nodes + 8 * (size_t)cur;
@@ -274,7 +293,7 @@ RT_D void trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const 
         const uint32_t ri = 4 * (first + k);
         F4 rec[4];
         if (LDS && recs_lds) {
-          const F4* q = lnodes + 8 * sc.n_nodes + ri;
+          const F4* q = lnodes + (W4 ? 8 : 4) * sc.n_nodes + ri;
           for (int e = 0; e < 4; ++e) rec[e] = ld_lds(q + e);
         } else {
           const F4* q = sc.leafprims + ri;

@@ -30,15 +30,15 @@
 
 namespace rt {
 
-// the whole BVH4 node array -> LDS (only used when 2 * n_nodes <= kLdsNodes
-// 64-B slots), then the leaf records when they fit too; returns whether they did
-RT_D bool stage_nodes(const Params& P, F4* lnodes) {
-  const int nl = min(P.sc.n_nodes, kLdsNodes / 2);
-  for (int i = threadIdx.x; i < 8 * nl; i += blockDim.x) lnodes[i] = P.sc.nodes[i];
+// the whole node array (W F4 per node) -> LDS (only used when it fits in
+// kLdsNodes 64-B slots), then the leaf records when they fit too
+RT_D bool stage_nodes(const Params& P, F4* lnodes, int W) {
+  const int nl = min(P.sc.n_nodes, 4 * kLdsNodes / W);
+  for (int i = threadIdx.x; i < W * nl; i += blockDim.x) lnodes[i] = P.sc.nodes[i];
   const bool recs = P.recs_lds != 0u;
   if (recs)
     for (int i = threadIdx.x; i < 4 * P.sc.n_refs; i += blockDim.x)
-      lnodes[8 * nl + i] = P.sc.leafprims[i];
+      lnodes[W * nl + i] = P.sc.leafprims[i];
   __syncthreads();
   return recs;
 }
@@ -78,7 +78,7 @@ template <bool LDS>
 __global__ __launch_bounds__(256) void k_extend(Params P, int it) {
   __shared__ F4 lnodes[LDS ? 4 * kLdsNodes : 4];
   __shared__ uint32_t lstack[kShortStack * 256];
-  const bool recs_lds = LDS && stage_nodes(P, lnodes);
+  const bool recs_lds = LDS && stage_nodes(P, lnodes, 8);
   const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
   const TravStack ts = {&lstack[threadIdx.x], P.ostack + gtid, P.stack_cols};
   const uint32_t sel = (uint32_t)it & 1u;
@@ -172,12 +172,12 @@ __global__ __launch_bounds__(256) void k_init(Params P) {
 // Waves per SIMD by feature set: the lean sets fit more waves in the register
 // file (VGPRs <= 512 / waves) and in LDS (28 KB static + the scene cache).
 constexpr int fused_waves(uint32_t ft) { return ft == 0u ? 5 : ft == FT_MEDIA ? 4 : 3; }
-template <bool LDS, uint32_t FT>
+template <bool LDS, uint32_t FT, bool W4>
 __global__ __launch_bounds__(256, fused_waves(FT)) void k_fused(Params P) {
   extern __shared__ F4 lnodes[];  // LDS scene cache, sized at launch (scene_lds_bytes)
   __shared__ uint32_t lstack[kShortStack * 256];
   __shared__ F4 lw[kLdsW * 256];
-  const bool recs_lds = LDS && stage_nodes(P, lnodes);
+  const bool recs_lds = LDS && stage_nodes(P, lnodes, W4 ? 8 : 4);
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;  // weight-stack column
   const TravStack ts = {&lstack[threadIdx.x], P.ostack + slot, P.stack_cols};
   const WStack ws = {&lw[threadIdx.x], kLdsW};
@@ -201,7 +201,8 @@ __global__ __launch_bounds__(256, fused_waves(FT)) void k_fused(Params P) {
     }
     if (!__any(has)) break;
     if (has && tr.cur != TRAV_DONE)
-      trav_steps<LDS, FT>(P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, tr, P.step_budget);
+      trav_steps<LDS, FT, W4>(P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, tr,
+                              P.step_budget);
     const bool ready = has && tr.cur == TRAV_DONE;
     const uint32_t n_ready = (uint32_t)__popcll(__ballot(ready));
     const bool busy = __any(has && !ready);
@@ -256,7 +257,10 @@ __global__ __launch_bounds__(256) void k_resolve(Params P, float* out, double sc
 struct DeviceScene {
   int device = -1;
   std::vector<void*> allocs;
-  DevScene d{};
+  DevScene d{};                 // nodes = BVH4
+  const F4* nodes2 = nullptr;   // BVH2 of the same leaves (tiny scenes)
+  uint32_t root2 = PRIM_NONE;
+  int32_t n_nodes2 = 0;
   ~DeviceScene() {
     for (void* p : allocs) (void)hipFree(p);
   }
@@ -397,6 +401,9 @@ static int ensure_scene(Scene* s, int device) {
   UP(h.tri, tri);
   UP(h.tri_attr, tri_attr);
   UP(h.nodes4, nodes);
+  if ((rc = upload(s->dev, h.nodes, &s->dev->nodes2)) != RT_OK) return rc;
+  s->dev->root2 = h.root;
+  s->dev->n_nodes2 = (int32_t)(h.nodes.size() / 4);
   UP(h.refs, refs);
   {
     std::vector<F4> recs;
@@ -483,10 +490,10 @@ static_assert(FT_SPHERE == RT_FT_SPHERE && FT_TRI == RT_FT_TRI && FT_METAL == RT
 template <bool LDS>
 static const void* fused_for(uint32_t set) {
   switch (set) {
-    case kFtSets[0]: return (const void*)k_fused<LDS, kFtSets[0]>;
-    case kFtSets[1]: return (const void*)k_fused<LDS, kFtSets[1]>;
-    case kFtSets[2]: return (const void*)k_fused<LDS, kFtSets[2]>;
-    default: return (const void*)k_fused<LDS, FT_ALL>;
+    case kFtSets[0]: return (const void*)k_fused<LDS, kFtSets[0], true>;
+    case kFtSets[1]: return (const void*)k_fused<LDS, kFtSets[1], true>;
+    case kFtSets[2]: return (const void*)k_fused<LDS, kFtSets[2], true>;
+    default: return (const void*)k_fused<LDS, FT_ALL, true>;
   }
 }
 static uint32_t pick_set(uint32_t feats) {
@@ -494,7 +501,11 @@ static uint32_t pick_set(uint32_t feats) {
     if ((feats & ~m) == 0u) return m;
   return FT_ALL;
 }
-static const void* pick_fused(bool lds, uint32_t set) {
+// BVH2 kernels exist for the two smallest sets with the tree in LDS (tiny scenes)
+static const void* pick_fused(bool lds, uint32_t set, bool w4) {
+  if (!w4 && lds && set == kFtSets[0]) return (const void*)k_fused<true, kFtSets[0], false>;
+  if (!w4 && lds && set == kFtSets[1]) return (const void*)k_fused<true, kFtSets[1], false>;
+  if (!w4) return nullptr;  // no such kernel: render_impl never asks (see w4 there)
   return lds ? fused_for<true>(set) : fused_for<false>(set);
 }
 
@@ -541,13 +552,24 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   // kernel's target waves per SIMD (160 KB per CU, 28 KB of stacks per group).
   // A tree that does not fit runs the global-node instantiation: caching only
   // its top measured 3-6 % slower on C3-C5 than one node source per kernel.
-  const size_t n_nodes = s->h.nodes4.size() / 8, n_refs = s->h.refs.size();  // BVH4
+  // Tree width: the fused kernel traverses the BVH4, except for tiny scenes
+  // (<= 64 leaf entries, C2's 18 quads) where the BVH2 measured 3 % faster;
+  // the wavefront extend kernel always takes the BVH4.
+  // BVH2 kernels exist only for the two smallest feature sets with the tree and
+  // its records in LDS (pick_fused): anything else takes the BVH4.
+  const size_t n_refs = s->h.refs.size();
   const size_t lds_slots = std::min<size_t>(
       kLdsNodes, (160u * 1024u / (unsigned)fused_waves(ft_set) - 28u * 1024u - 512u) / 64u);
-  const bool f_lds = 2 * n_nodes <= lds_slots;
-  const void* fused_kernel = pick_fused(f_lds, ft_set);
-  const size_t fused_lds =
-      f_lds ? 64 * (2 * n_nodes + (2 * n_nodes + n_refs <= lds_slots ? n_refs : 0)) : 0;
+  const bool w4 = mode == RT_MODE_WAVEFRONT || n_refs > 64 || s->h.nodes.empty() ||
+                  (ft_set != kFtSets[0] && ft_set != kFtSets[1]) ||
+                  s->h.nodes.size() / 4 + n_refs > lds_slots;
+  const size_t n_nodes = w4 ? s->h.nodes4.size() / 8 : s->h.nodes.size() / 4;
+  const size_t node_slots = w4 ? 2 : 1;  // 64-B LDS slots per node
+  const bool f_lds = node_slots * n_nodes <= lds_slots;
+  const bool f_recs = f_lds && node_slots * n_nodes + n_refs <= lds_slots;
+  const void* fused_kernel = pick_fused(f_lds, ft_set, w4);
+  if (!fused_kernel) return set_error(RT_ERR_UNSUPPORTED, "internal: no fused kernel for this scene");
+  const size_t fused_lds = f_lds ? 64 * (node_slots * n_nodes + (f_recs ? n_refs : 0)) : 0;
   if (mode == RT_MODE_FUSED) {
     if ((rc = occupancy_blocks(fused_kernel, o.device, &fused_blocks, fused_lds))) return rc;
     if (o.path_slots > 0) fused_blocks = std::max(1, std::min(fused_blocks, (o.path_slots + 255) / 256));
@@ -588,6 +610,11 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
 
   Params p{};
   p.sc = s->dev->d;
+  if (!w4) {
+    p.sc.nodes = s->dev->nodes2;
+    p.sc.root = s->dev->root2;
+    p.sc.n_nodes = s->dev->n_nodes2;
+  }
   for (int i = 0; i < 3; ++i) {
     p.p00r[i] = (float)(cd.pixel00[i] - cd.center[i]);
     p.du[i] = (float)cd.delta_u[i];
@@ -618,7 +645,7 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   // shading every round; shallow trees (C2, C3) lose 3-30 % from any bound.
   p.step_budget = env_int("RT_STEP_BUDGET", n_nodes > 6000 ? 6 : (1 << 30));
   p.shade_min = (uint32_t)env_int("RT_SHADE_MIN", 1);
-  p.recs_lds = f_lds && 2 * n_nodes + n_refs <= lds_slots ? 1u : 0u;
+  p.recs_lds = f_recs ? 1u : 0u;
   p.seed = o.seed;
   p.ray_o = st->ray_o;
   p.ray_d = st->ray_d;
