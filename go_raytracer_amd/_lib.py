@@ -83,6 +83,7 @@ class RtStats(C.Structure):
         ("rows", C.c_int32), ("mode", C.c_int32), ("path_slots", C.c_int32),
         ("ms_fused", C.c_double),
         ("kernel_features", C.c_int32), ("scene_features", C.c_int32),
+        ("tree_width", C.c_int32), ("lds_scene", C.c_int32),
     ]
 
 

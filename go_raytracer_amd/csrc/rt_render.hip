@@ -782,6 +782,8 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     stats->path_slots = (int32_t)P;
     stats->kernel_features = mode == RT_MODE_FUSED ? (int32_t)ft_set : (int32_t)FT_ALL;
     stats->scene_features = (int32_t)feats;
+    stats->tree_width = w4 ? 4 : 2;
+    stats->lds_scene = mode == RT_MODE_FUSED ? (f_lds ? 1 : 0) : (lds_nodes ? 1 : 0);
     auto sum_ms = [&](const std::vector<std::pair<int, int>>& v, double* acc) -> int {
       for (auto& pr : v) {
         float ms = 0;

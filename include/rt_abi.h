@@ -296,6 +296,8 @@ typedef struct {
   double ms_fused;       /* fused-kernel time (RT_FLAG_PROFILE) */
   int32_t kernel_features; /* RT_FT_* set compiled into the fused kernel that ran */
   int32_t scene_features;  /* RT_FT_* set the scene needs */
+  int32_t tree_width;      /* BVH arity the kernels traversed (2 or 4) */
+  int32_t lds_scene;       /* 1: nodes (and leaf records) ran from the LDS cache */
 } rt_stats;
 
 /* Render this rank's rows; out_rgb (host) receives linear mean RGB

@@ -46,6 +46,8 @@ FULL = [
     # BASELINE.json configs at full size; the oracle checks every `stride`-th row
     ("cornell", 800, 1024, 1.0, 100),   # C2
     ("book1", 1200, 512, 1.5, 160),     # C3 (aspect 1.5 -> 800 rows, 484 spp)
+    ("book2", 800, 4096, 1.0, 100),     # C4 (one GPU here; the 8-GPU split is rank-invariant)
+    ("model", 1920, 1024, 16 / 9, 216),  # C5 (1M-triangle substitute mesh, 1920x1080)
 ]
 
 
@@ -64,3 +66,23 @@ def test_full_size_parity_on_row_subsample(rt, oracle, gpu, name, width, spp, as
     assert abs(m["mean_gpu"] - m["mean_ref"]) <= 2e-3 * max(1.0, abs(m["mean_ref"]))
     seg_ratio = (st["segments"] / st["samples"]) / (ost["segments"] / ost["samples"])
     assert abs(seg_ratio - 1) < 0.01
+
+
+# kernel choice (DESIGN.md "Kernels"): the compiled feature set covers the
+# scene's, C2 runs the lean set on its binary tree from LDS, large scenes the BVH4
+@pytest.mark.parametrize("name,width,lean,width_tree,lds", [
+    ("cornell", 64, True, 2, 1), ("book1", 64, False, 4, None), ("book2", 64, False, 4, 0),
+    ("model:256x32", 64, False, 4, 0), ("cornell_smoke", 64, False, None, 1)])
+def test_kernel_selection(rt, gpu, name, width, lean, width_tree, lds):
+    t, cam, w, l = _scene(rt, name, width, 4)
+    with rt.Scene(t, w, l) as sc:
+        _, st = sc.render(cam, seed=1, mode="fused")
+        info = sc.info()
+    assert st["scene_features"] == info["features"]
+    assert st["kernel_features"] & st["scene_features"] == st["scene_features"]
+    if lean:
+        assert st["kernel_features"] == 0
+    if width_tree is not None:
+        assert st["tree_width"] == width_tree
+    if lds is not None:
+        assert st["lds_scene"] == lds
