@@ -88,7 +88,7 @@ RT_D f3 refract(f3 v, f3 n, float eta) {
 // clampContribution camera.go:334-341
 RT_D f3 clamp_contribution(f3 c, float maxv) {
   float intensity = c.x + c.y + c.z;
-  if (intensity > maxv) return c * (maxv / intensity);
+  if (intensity > maxv) return c * (maxv * rcp(intensity));
   return c;
 }
 

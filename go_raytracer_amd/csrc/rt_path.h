@@ -469,7 +469,7 @@ RT_D f3 tri_normal(const DevScene& sc, uint32_t idx, float bu, float bv) {
 
 // light PdfValue: sphere objects.go:52-62, quad :152-160, triangle :356-367
 template <uint32_t FT>
-RT_D float prim_pdf(const DevScene& sc, uint32_t ref, f3 origin, f3 dir) {
+RT_D float prim_pdf(const DevScene& sc, uint32_t ref, int li, f3 origin, f3 dir) {
   uint32_t type = ref >> 30, idx = ref & 0x3FFFFFFFu;
   if (HAS(FT_SPHERE) && type == PRIM_SPHERE) {
     float t;
@@ -483,10 +483,12 @@ RT_D float prim_pdf(const DevScene& sc, uint32_t ref, f3 origin, f3 dir) {
   float t, u, v, area;
   f3 n;
   if (!HAS(FT_TRI) || type == PRIM_QUAD) {
-    if (!hit_quad(sc, idx, origin, dir, 0.001f, kInf, t, u, v)) return 0.0f;
-    const F4* q = sc.quad + 5 * (size_t)idx;
-    n = xyz(q[3]);
-    area = q[1].w;
+    // the light's leaf-record copy: 4 loads and the traversal's quad test
+    const F4* lr = sc.light_recs + 4 * (size_t)li;
+    const F4 rec[4] = {lr[0], lr[1], lr[2], lr[3]};
+    if (!hit_quad_rec(rec, origin, dir, 0.001f, kInf, t, u, v)) return 0.0f;
+    n = xyz(rec[1]);
+    area = rec[2].w;
   } else {
     if (!hit_tri(sc, idx, origin, dir, 0.001f, kInf, t, u, v)) return 0.0f;
     n = tri_normal(sc, idx, u, v);
@@ -504,7 +506,7 @@ RT_D float lights_pdf(const DevScene& sc, f3 origin, f3 dir) {
   for (int i = 0; i < sc.n_lights; ++i) {
     const DevLight L = sc.lights[i];
     if (L.ref == PRIM_NONE) continue;
-    sum += L.weight * prim_pdf<FT>(sc, L.ref, origin, dir);
+    sum += L.weight * prim_pdf<FT>(sc, L.ref, i, origin, dir);
   }
   return sum;
 }
@@ -570,6 +572,7 @@ struct Path {
   f3 o, d;
   float time;
   uint32_t chunk, j, k, nst, flags;
+  uint32_t gpix, s0;  // global pixel and first sample of the chunk (chunk_ids, cached)
   f3 pend, pre, acc;
   uint32_t segs, pushes;  // per-lane statistics (fused kernel)
 };
@@ -613,6 +616,21 @@ struct WStack {
     if ((int)k < nlds) st_lds(lds + k * 256, v);
     else st_glb(P.stack + (size_t)(k - nlds) * P.P + slot, v);
   }
+  // backward clamp fold over entries nst-1 .. 0 (camera.go:328-330): the HBM
+  // entries (rare) one by one, the LDS entries read together and applied unrolled
+  RT_D f3 fold(const Params& P, uint32_t slot, uint32_t nst, f3 L) const {
+    for (int k = (int)nst - 1; k >= nlds; --k)
+      L = clamp_contribution(xyz(ld_glb(P.stack + (size_t)(k - nlds) * P.P + slot)) * L, P.maxc);
+    if (nlds > 0 && nst > 0) {
+      F4 e[kLdsW];
+#pragma unroll
+      for (int i = 0; i < kLdsW; ++i) e[i] = ld_lds(lds + i * 256);  // unused ones are garbage
+#pragma unroll
+      for (int i = kLdsW - 1; i >= 0; --i)
+        if (i < (int)nst) L = clamp_contribution(xyz(e[i]) * L, P.maxc);
+    }
+    return L;
+  }
   RT_D F4 get(const Params& P, uint32_t slot, uint32_t k) const {
     F4 v;
     if ((int)k < nlds) {
@@ -641,6 +659,9 @@ RT_D void load_path(const Params& P, uint32_t slot, Path& s) {
   s.time = ro.w;
   s.d = xyz(rd);
   s.chunk = ps.x;
+  const Ids id = chunk_ids(P, s.chunk);
+  s.gpix = id.gpix;
+  s.s0 = id.sample0;
   s.j = ps.y & 0xFFFu;
   s.k = (ps.y >> 12) & 0xFFu;
   s.nst = (ps.y >> 20) & 0xFFu;
@@ -653,6 +674,8 @@ RT_D void start_sample(const Params& P, uint32_t slot, Path& s, uint32_t chunk, 
   Ids id = chunk_ids(P, chunk);
   camera_ray(P, id, id.sample0 + j, s.o, s.d, s.time);
   s.chunk = chunk;
+  s.gpix = id.gpix;
+  s.s0 = id.sample0;
   s.j = j;
   s.k = 0;
   s.nst = 0;
@@ -728,8 +751,7 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
       lterm = ff ? tex_value<FT>(sc, M.tex, u, v, p) : mk3(0, 0, 0);
       term = true;
     } else {
-      const Ids id = chunk_ids(P, s.chunk);
-      const rt_u32x4 r = rt_rng_draw(P.seed, id.gpix, id.sample0 + s.j, RT_STREAM(s.k, 0));
+      const rt_u32x4 r = rt_rng_draw(P.seed, s.gpix, s.s0 + s.j, RT_STREAM(s.k, 0));
       f3 ndir;
       bool clamp_vertex = false;
       f3 weight;
@@ -814,15 +836,14 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
   const bool zero = lterm.x == 0.0f && lterm.y == 0.0f && lterm.z == 0.0f;
   if (!(zero && !(s.flags & F_NONFINITE))) {
     if (s.flags & F_PEND) L = clamp_contribution(get_pend<SOA>(P, slot, s) * L, P.maxc);
-    for (int kk = (int)s.nst - 1; kk >= 0; --kk)
-      L = clamp_contribution(xyz(ws.get(P, slot, (uint32_t)kk)) * L, P.maxc);
+    L = ws.fold(P, slot, s.nst, L);
     if (s.flags & F_PRE) L = get_pre<SOA>(P, slot, s) * L;
   } else {
     L = mk3(0, 0, 0);
   }
   f3 acc = L;
   if (s.j > 0) acc = get_acc<SOA>(P, slot, s) + L;
-  const uint32_t count = chunk_ids(P, s.chunk).count;
+  const uint32_t count = min(P.K, P.ss - s.s0);  // chunk_ids().count
   if (s.j + 1 < count) {
     set_acc<SOA>(P, slot, s, acc);
     start_sample<SOA>(P, slot, s, s.chunk, s.j + 1);

@@ -44,8 +44,7 @@ RT_D bool stage_nodes(const Params& P, F4* lnodes, int W) {
 }
 
 RT_D void record_trace(const Params& P, const Path& s, const Hit& best) {
-  const Ids id = chunk_ids(P, s.chunk);
-  if (id.gpix == P.trace_gpix && id.sample0 + s.j == P.trace_sample && (int)s.k < P.trace_cap) {
+  if (s.gpix == P.trace_gpix && s.s0 + s.j == P.trace_sample && (int)s.k < P.trace_cap) {
     P.trace[3 * s.k + 0] = {s.o.x, s.o.y, s.o.z, s.time};
     P.trace[3 * s.k + 1] = {s.d.x, s.d.y, s.d.z, (float)s.k};
     P.trace[3 * s.k + 2] = {best.t, best.u, best.v, bitsf(best.ref)};
@@ -55,10 +54,8 @@ RT_D void record_trace(const Params& P, const Path& s, const Hit& best) {
 // media + debug trace on top of the world closest hit, camera.go:300
 template <uint32_t FT>
 RT_D void finish_hit(const Params& P, const Path& s, Hit& best) {
-  if (HAS(FT_MEDIA) && P.sc.n_media > 0) {
-    const Ids id = chunk_ids(P, s.chunk);
-    trace_media(P, s.o, s.d, s.time, 0.001f, id.gpix, id.sample0 + s.j, s.k, best);
-  }
+  if (HAS(FT_MEDIA) && P.sc.n_media > 0)
+    trace_media(P, s.o, s.d, s.time, 0.001f, s.gpix, s.s0 + s.j, s.k, best);
   if (P.trace) record_trace(P, s, best);
 }
 
@@ -333,11 +330,24 @@ static FastDiv make_fastdiv(uint32_t d) {
 }
 
 // the traversal's leaf records (rt_device.h "leaf records"), in refs order
+static void make_record(const HostScene& h, uint32_t ref, F4* r);
 static void build_leaf_records(const HostScene& h, std::vector<F4>& recs) {
   recs.assign(4 * h.refs.size(), F4{0, 0, 0, 0});
-  for (size_t i = 0; i < h.refs.size(); ++i) {
-    const uint32_t ref = h.refs[i], type = ref >> 30, idx = ref & 0x3FFFFFFFu;
-    F4* r = &recs[4 * i];
+  for (size_t i = 0; i < h.refs.size(); ++i) make_record(h, h.refs[i], &recs[4 * i]);
+}
+// light table entries: quad lights as leaf records with the area in [2].w (prim_pdf)
+static void build_light_records(const HostScene& h, std::vector<F4>& recs) {
+  recs.assign(4 * std::max<size_t>(h.lights.size(), 1), F4{0, 0, 0, 0});
+  for (size_t i = 0; i < h.lights.size(); ++i) {
+    const uint32_t ref = h.lights[i].ref;
+    if (ref == PRIM_NONE || (ref >> 30) != PRIM_QUAD) continue;
+    make_record(h, ref, &recs[4 * i]);
+    recs[4 * i + 2].w = h.quad[5 * (size_t)(ref & 0x3FFFFFFFu) + 1].w;  // area
+  }
+}
+static void make_record(const HostScene& h, uint32_t ref, F4* r) {
+  {
+    const uint32_t type = ref >> 30, idx = ref & 0x3FFFFFFFu;
     float rb;
     memcpy(&rb, &ref, 4);
     if (type == PRIM_SPHERE) {
@@ -406,9 +416,11 @@ static int ensure_scene(Scene* s, int device) {
   s->dev->n_nodes2 = (int32_t)(h.nodes.size() / 4);
   UP(h.refs, refs);
   {
-    std::vector<F4> recs;
+    std::vector<F4> recs, lrecs;
     build_leaf_records(h, recs);
     UP(recs, leafprims);
+    build_light_records(h, lrecs);
+    UP(lrecs, light_recs);
   }
   UP(h.media, media);
   UP(h.medium_refs, medium_refs);
