@@ -10,7 +10,7 @@ namespace rt {
 
 constexpr int kLdsNodes = 384;   // 64-B slots staged in LDS per workgroup (24 KB): BVH nodes,
                                  // then the leaf records when both fit (LDS instantiation)
-constexpr int kLdsW = 4;         // clamp-weight stack entries per lane kept in LDS (fused)
+constexpr int kLdsWMax = 4;      // clamp-weight stack entries per lane kept in LDS (fused, max)
 constexpr int kStack = 64;       // traversal stack entries per lane (LDS short stack + HBM overflow)
 constexpr int kShortStack = 12;  // LDS entries per lane (column layout: [entry][thread])
 constexpr int kMaxIt = 1 << 16;  // per-iteration counter slots (no per-iteration memsets)
@@ -622,12 +622,13 @@ struct WStack {
     for (int k = (int)nst - 1; k >= nlds; --k)
       L = clamp_contribution(xyz(ld_glb(P.stack + (size_t)(k - nlds) * P.P + slot)) * L, P.maxc);
     if (nlds > 0 && nst > 0) {
-      F4 e[kLdsW];
+      F4 e[kLdsWMax];
 #pragma unroll
-      for (int i = 0; i < kLdsW; ++i) e[i] = ld_lds(lds + i * 256);  // unused ones are garbage
+      for (int i = 0; i < kLdsWMax; ++i)
+        if (i < nlds) e[i] = ld_lds(lds + i * 256);  // entries >= nst are garbage, unused
 #pragma unroll
-      for (int i = kLdsW - 1; i >= 0; --i)
-        if (i < (int)nst) L = clamp_contribution(xyz(e[i]) * L, P.maxc);
+      for (int i = kLdsWMax - 1; i >= 0; --i)
+        if (i < nlds && i < (int)nst) L = clamp_contribution(xyz(e[i]) * L, P.maxc);
     }
     return L;
   }

@@ -167,17 +167,23 @@ __global__ __launch_bounds__(256) void k_init(Params P) {
 // ----------------------------------------------------------------- fused ---
 // FT = compiled-in scene features (rt_device.h), chosen per scene by pick_fused.
 // Waves per SIMD by feature set: the lean sets fit more waves in the register
-// file (VGPRs <= 512 / waves) and in LDS (28 KB static + the scene cache).
-constexpr int fused_waves(uint32_t ft) { return ft == 0u ? 5 : ft == FT_MEDIA ? 4 : 3; }
+// file (VGPRs <= 512 / waves) and in LDS (24 KB static + the scene cache).
+constexpr int fused_waves(uint32_t ft) { return ft == 0u ? 6 : ft == FT_MEDIA ? 4 : 3; }
+// LDS weight-stack entries: 3 for the 6-wave lean kernel (its LDS budget), 4 elsewhere
+// (book2's longer paths: 3 entries cost it 5 %)
+constexpr int fused_wlds(uint32_t ft) { return ft == 0u ? 3 : 4; }
+constexpr unsigned fused_static_lds(uint32_t ft) {
+  return (unsigned)(kShortStack * 4 + fused_wlds(ft) * 16) * 256u;
+}
 template <bool LDS, uint32_t FT, bool W4>
 __global__ __launch_bounds__(256, fused_waves(FT)) void k_fused(Params P) {
   extern __shared__ F4 lnodes[];  // LDS scene cache, sized at launch (scene_lds_bytes)
   __shared__ uint32_t lstack[kShortStack * 256];
-  __shared__ F4 lw[kLdsW * 256];
+  __shared__ F4 lw[fused_wlds(FT) * 256];
   const bool recs_lds = LDS && stage_nodes(P, lnodes, W4 ? 8 : 4);
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;  // weight-stack column
   const TravStack ts = {&lstack[threadIdx.x], P.ostack + slot, P.stack_cols};
-  const WStack ws = {&lw[threadIdx.x], kLdsW};
+  const WStack ws = {&lw[threadIdx.x], fused_wlds(FT)};
   Path s;
   s.segs = 0;
   s.pushes = 0;
@@ -561,7 +567,7 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   const uint32_t feats = scene_features(s->h), ft_set = pick_set(feats);
   // The fused kernel's LDS scene cache (stage_nodes): all BVH nodes, then the
   // leaf records when both fit, within the LDS a workgroup may take at the
-  // kernel's target waves per SIMD (160 KB per CU, 28 KB of stacks per group).
+  // kernel's target waves per SIMD (160 KB per CU, 24 KB of stacks per group).
   // A tree that does not fit runs the global-node instantiation: caching only
   // its top measured 3-6 % slower on C3-C5 than one node source per kernel.
   // Tree width: the fused kernel traverses the BVH4, except for tiny scenes
@@ -571,7 +577,8 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   // its records in LDS (pick_fused): anything else takes the BVH4.
   const size_t n_refs = s->h.refs.size();
   const size_t lds_slots = std::min<size_t>(
-      kLdsNodes, (160u * 1024u / (unsigned)fused_waves(ft_set) - 28u * 1024u - 512u) / 64u);
+      kLdsNodes,
+      (160u * 1024u / (unsigned)fused_waves(ft_set) - fused_static_lds(ft_set) - 512u) / 64u);
   const bool w4 = mode == RT_MODE_WAVEFRONT || n_refs > 64 || s->h.nodes.empty() ||
                   (ft_set != kFtSets[0] && ft_set != kFtSets[1]) ||
                   s->h.nodes.size() / 4 + n_refs > lds_slots;

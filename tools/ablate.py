@@ -44,6 +44,19 @@ V = {
         "    if (s.flags & F_PRE) L = get_pre<SOA>(P, slot, s) * L;",
         "    if (s.flags & F_PRE) L = get_pre<SOA>(P, slot, s) * L;\n"
         "    { f3 L2 = L * 1.0000001f; for (int kk = (int)s.nst - 1; kk >= 0; --kk) L2 = clamp_contribution(xyz(ws.get(P, slot, (uint32_t)kk)) * L2, P.maxc); L = L + L2 * 0.0f; }")],
+    "waves6": [("go_raytracer_amd/csrc/rt_render.hip",
+        "constexpr int fused_waves(uint32_t ft) { return ft == 0u ? 5 : ft == FT_MEDIA ? 4 : 3; }",
+        "constexpr int fused_waves(uint32_t ft) { return ft == 0u ? 6 : ft == FT_MEDIA ? 4 : 3; }"),
+        ("go_raytracer_amd/csrc/rt_path.h", "constexpr int kLdsW = 4;", "constexpr int kLdsW = 3;"),
+        ("go_raytracer_amd/csrc/rt_render.hip", "- 28u * 1024u - 512u) / 64u);", "- 24u * 1024u - 512u) / 64u);")],
+    "stack8": [("go_raytracer_amd/csrc/rt_path.h", "constexpr int kShortStack = 12;", "constexpr int kShortStack = 8;"),
+        ("go_raytracer_amd/csrc/rt_render.hip", "- 28u * 1024u - 512u) / 64u);", "- 24u * 1024u - 512u) / 64u);")],
+    "waves7": [("go_raytracer_amd/csrc/rt_render.hip",
+        "constexpr int fused_waves(uint32_t ft) { return ft == 0u ? 5 : ft == FT_MEDIA ? 4 : 3; }",
+        "constexpr int fused_waves(uint32_t ft) { return ft == 0u ? 7 : ft == FT_MEDIA ? 4 : 3; }"),
+        ("go_raytracer_amd/csrc/rt_path.h", "constexpr int kLdsW = 4;", "constexpr int kLdsW = 3;"),
+        ("go_raytracer_amd/csrc/rt_path.h", "constexpr int kShortStack = 12;", "constexpr int kShortStack = 8;"),
+        ("go_raytracer_amd/csrc/rt_render.hip", "- 28u * 1024u - 512u) / 64u);", "- 20u * 1024u - 512u) / 64u);")],
 }
 names = sys.argv[1:] or list(V)
 for name in names:
