@@ -168,7 +168,9 @@ __global__ __launch_bounds__(256) void k_init(Params P) {
 // FT = compiled-in scene features (rt_device.h), chosen per scene by pick_fused.
 // Waves per SIMD by feature set: the lean sets fit more waves in the register
 // file (VGPRs <= 512 / waves) and in LDS (24 KB static + the scene cache).
-constexpr int fused_waves(uint32_t ft) { return ft == 0u ? 6 : ft == FT_MEDIA ? 4 : 3; }
+constexpr int fused_waves(uint32_t ft) {
+  return ft == 0u ? 6 : ft == FT_MEDIA ? 4 : ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? 4 : 3;
+}
 // LDS weight-stack entries: 3 for the 6-wave lean kernel (its LDS budget), 4 elsewhere
 // (book2's longer paths: 3 entries cost it 5 %)
 constexpr int fused_wlds(uint32_t ft) { return ft == 0u ? 3 : 4; }

@@ -30,10 +30,14 @@ V = {
         "  rt_u32x4 r = rt_rng_draw(P.seed, id.gpix, sample, RT_STREAM_CAMERA);",
         "  rt_u32x4 r = {{sample * 0x9E3779B1u, sample * 0x85EBCA77u, sample * 0xC2B2AE3Du, 0u}};")],
     "dbl_trav": [("go_raytracer_amd/csrc/rt_render.hip",
-        "      trav_steps<LDS, FT>(P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, tr, P.step_budget);",
-        "    { Trav t2 = tr; trav_steps<LDS, FT>(P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, t2, P.step_budget);\n"
-        "      trav_steps<LDS, FT>(P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, tr, P.step_budget);\n"
+        "      trav_steps<LDS, FT, W4>(P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, tr,\n                              P.step_budget);",
+        "    { Trav t2 = tr; trav_steps<LDS, FT, W4>(P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, t2, P.step_budget);\n"
+        "      trav_steps<LDS, FT, W4>(P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, tr, P.step_budget);\n"
         "      tr.best.t = fminf(tr.best.t, t2.best.t + 0.0f * tr.best.t); }")],
+    "dbl_media": [("go_raytracer_amd/csrc/rt_render.hip",
+        "    trace_media(P, s.o, s.d, s.time, 0.001f, s.gpix, s.s0 + s.j, s.k, best);",
+        "  { Hit b2 = best; trace_media(P, s.o, s.d, s.time, 0.001f, s.gpix, s.s0 + s.j, s.k, b2);\n"
+        "    trace_media(P, s.o, s.d, s.time, 0.001f, s.gpix, s.s0 + s.j, s.k, best); best.t = fminf(best.t, b2.t + 0.0f * best.t); }")],
     "dbl_lightpdf": [("go_raytracer_amd/csrc/rt_path.h",
         "        float pdf = 0.5f * lights_pdf<FT>(sc, p, ndir) + 0.5f * bsdf_pdf;",
         "        float pdf = 0.25f * (lights_pdf<FT>(sc, p, ndir) + lights_pdf<FT>(sc, p, ndir * 1.0000001f)) + 0.5f * bsdf_pdf;")],
@@ -57,6 +61,15 @@ V = {
         ("go_raytracer_amd/csrc/rt_path.h", "constexpr int kLdsW = 4;", "constexpr int kLdsW = 3;"),
         ("go_raytracer_amd/csrc/rt_path.h", "constexpr int kShortStack = 12;", "constexpr int kShortStack = 8;"),
         ("go_raytracer_amd/csrc/rt_render.hip", "- 28u * 1024u - 512u) / 64u);", "- 20u * 1024u - 512u) / 64u);")],
+    "set47w4": [("go_raytracer_amd/csrc/rt_render.hip",
+        "constexpr int fused_waves(uint32_t ft) { return ft == 0u ? 6 : ft == FT_MEDIA ? 4 : 3; }",
+        "constexpr int fused_waves(uint32_t ft) { return ft == 0u ? 6 : (ft == FT_MEDIA || ft == 47u) ? 4 : 3; }")],
+    "allw4": [("go_raytracer_amd/csrc/rt_render.hip",
+        "ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? 4 : 3;",
+        "ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? 4 : 4;")],
+    "medw5": [("go_raytracer_amd/csrc/rt_render.hip",
+        "return ft == 0u ? 6 : ft == FT_MEDIA ? 4 :",
+        "return ft == 0u ? 6 : ft == FT_MEDIA ? 5 :")],
 }
 names = sys.argv[1:] or list(V)
 for name in names:
