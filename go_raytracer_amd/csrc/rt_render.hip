@@ -661,11 +661,13 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   p.fd_npix = make_fastdiv(npix);
   p.fd_width = make_fastdiv(W);
   p.fd_s = make_fastdiv((uint32_t)cd.spp_sqrt);
-  // Measured on the full-size configs (tools/sched_sweep.py, profiles/): deep
-  // trees (C5, 1M triangles) gain ~45 % from bounded rounds of 8-12 steps with
-  // shading every round; shallow trees (C2, C3) lose 3-30 % from any bound.
-  p.step_budget = env_int("RT_STEP_BUDGET", n_nodes > 6000 ? 6 : (1 << 30));
-  p.shade_min = (uint32_t)env_int("RT_SHADE_MIN", 1);
+  // Scheduling rounds, measured on the full-size configs (tools/sched_sweep.py,
+  // profiles/r1_sched_sweep*.jsonl): trees read through L1/L2 gain from bounded
+  // rounds of 8 steps (C5 +75 %, C4 +10 %) so short rays do not idle behind long
+  // ones; LDS-resident trees (C2, C3) lose from any bound.  The all-features
+  // kernel, whose shading is long, also gains from shading 32+ lanes at once.
+  p.step_budget = env_int("RT_STEP_BUDGET", f_lds ? (1 << 30) : 8);
+  p.shade_min = (uint32_t)env_int("RT_SHADE_MIN", !f_lds && ft_set == FT_ALL ? 32 : 1);
   p.recs_lds = f_recs ? 1u : 0u;
   p.seed = o.seed;
   p.ray_o = st->ray_o;
