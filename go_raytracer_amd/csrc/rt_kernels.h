@@ -198,15 +198,18 @@ RT_D bool hit_sphere_rec(const F4 r[4], f3 o, f3 d, float time, float tmin, floa
   double c = ox * ox + oy * oy + oz * oz - rr * rr;
   double disc = h * h - a * c;
   if (disc < 0) return false;
-  double sq = sqrt(disc);
-  // (tmin < (h -/+ sq)/a < tmax) tested as tmin*a < q < tmax*a (a > 0): one division
+  // fp64 sqrt as v_sqrt_f64 (~2^-23 relative) + one Newton step (~1e-14): the
+  // exact-rounding library sequence is twice as long and buys nothing here
+  double sq = __builtin_amdgcn_sqrt(disc);
+  sq = disc > 0.0 ? fma(0.5 * fma(-sq, sq, disc), __builtin_amdgcn_rcp(sq), sq) : 0.0;
+  // (tmin < (h -/+ sq)/a < tmax) tested as tmin*a < q < tmax*a (a > 0): no division
   double lo = (double)tmin * a, hi = (double)tmax * a;
   double q = h - sq;
   if (!(lo < q && q < hi)) {
     q = h + sq;
     if (!(lo < q && q < hi)) return false;
   }
-  t_out = (float)(q / a);
+  t_out = (float)(q * __builtin_amdgcn_rcp(a));  // fp32-level result from fp64 q: float t
   return true;
 }
 RT_D bool hit_quad_rec(const F4 r[4], f3 o, f3 d, float tmin, float tmax, float& t_out,
