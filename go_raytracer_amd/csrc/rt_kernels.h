@@ -110,10 +110,15 @@ RT_D bool hit_sphere_d(const DevScene& sc, uint32_t i, f3 o, f3 d, float time, d
   double c = ox * ox + oy * oy + oz * oz - r * r;
   double disc = h * h - a * c;
   if (disc < 0) return false;
-  double sq = sqrt(disc);
-  double root = (h - sq) / a;
+  // v_sqrt_f64 / v_rcp_f64 (~2^-23 relative) + one Newton step each (~1e-14):
+  // fp64-grade roots (media need |t| ~ 1e4 to 1e-4) without the library sequences
+  double sq = __builtin_amdgcn_sqrt(disc);
+  sq = disc > 0.0 ? fma(0.5 * fma(-sq, sq, disc), __builtin_amdgcn_rcp(sq), sq) : 0.0;
+  double ia = __builtin_amdgcn_rcp(a);
+  ia = fma(ia, fma(-a, ia, 1.0), ia);
+  double root = (h - sq) * ia;
   if (!(tmin < root && root < tmax)) {
-    root = (h + sq) / a;
+    root = (h + sq) * ia;
     if (!(tmin < root && root < tmax)) return false;
   }
   t_out = root;
