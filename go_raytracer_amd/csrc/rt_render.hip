@@ -554,12 +554,6 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   const uint32_t rows = H > (uint32_t)o.rank ? (H - (uint32_t)o.rank + o.nranks - 1) / o.nranks : 0;
   const uint32_t npix = rows * W;
   const uint32_t ss = (uint32_t)cd.spp_sqrt * (uint32_t)cd.spp_sqrt;
-  uint32_t K = o.chunk > 0 ? (uint32_t)o.chunk : std::min<uint32_t>(ss, 32u);
-  K = std::min<uint32_t>(std::min(K, ss), 4096u);
-  const uint32_t cpp = (ss + K - 1) / K;
-  const uint64_t n_chunks64 = (uint64_t)npix * cpp;
-  if (n_chunks64 >= 0xF0000000ull) return set_error(RT_ERR_UNSUPPORTED, "too many work chunks");
-  const uint32_t n_chunks = (uint32_t)n_chunks64;
   int mode = o.mode;
   if (mode != RT_MODE_WAVEFRONT && mode != RT_MODE_FUSED) mode = RT_MODE_FUSED;
   const int depth_cap = cd.max_depth + 1;
@@ -595,7 +589,30 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     if ((rc = occupancy_blocks(fused_kernel, o.device, &fused_blocks, fused_lds))) return rc;
     if (o.path_slots > 0) fused_blocks = std::max(1, std::min(fused_blocks, (o.path_slots + 255) / 256));
     P = (uint32_t)fused_blocks * 256u;
-  } else {
+  }
+  // Samples per chunk.  Fused: the largest K in {32, 16, 8} that still gives
+  // every lane >= 48 chunks (tree in LDS) or >= 128 (tree through L1/L2, whose
+  // per-pixel cost varies more), so the last chunks do not leave most lanes idle:
+  // one GPU's share of an 8-GPU C2 runs 12 % faster at K = 8 than at 32, C5 37 %
+  // (tools/chunk_sweep.py, profiles/r1_chunk_sweep.jsonl); full one-GPU configs keep 32.
+  uint32_t K = 32u;
+  if (o.chunk > 0) {
+    K = (uint32_t)o.chunk;
+  } else if (mode == RT_MODE_FUSED) {
+    const uint64_t work = (uint64_t)npix * ss, need = (uint64_t)(f_lds ? 48u : 128u) * P;
+    K = 8u;
+    for (uint32_t k : {32u, 16u})
+      if (work / k >= need) {
+        K = k;
+        break;
+      }
+  }
+  K = std::max<uint32_t>(1u, std::min<uint32_t>(std::min(K, ss), 4096u));
+  const uint32_t cpp = (ss + K - 1) / K;
+  const uint64_t n_chunks64 = (uint64_t)npix * cpp;
+  if (n_chunks64 >= 0xF0000000ull) return set_error(RT_ERR_UNSUPPORTED, "too many work chunks");
+  const uint32_t n_chunks = (uint32_t)n_chunks64;
+  if (mode != RT_MODE_FUSED) {
     P = o.path_slots > 0 ? (uint32_t)o.path_slots : (1u << 20);
     P = std::max<uint32_t>(256u, std::min<uint32_t>(P, std::max<uint32_t>(n_chunks, 256u)));
     P = (P + 255u) & ~255u;
@@ -806,6 +823,7 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     stats->kernel_features = mode == RT_MODE_FUSED ? (int32_t)ft_set : (int32_t)FT_ALL;
     stats->scene_features = (int32_t)feats;
     stats->tree_width = w4 ? 4 : 2;
+    stats->chunk_samples = (int32_t)K;
     stats->lds_scene = mode == RT_MODE_FUSED ? (f_lds ? 1 : 0) : (lds_nodes ? 1 : 0);
     auto sum_ms = [&](const std::vector<std::pair<int, int>>& v, double* acc) -> int {
       for (auto& pr : v) {

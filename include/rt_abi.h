@@ -298,6 +298,8 @@ typedef struct {
   int32_t scene_features;  /* RT_FT_* set the scene needs */
   int32_t tree_width;      /* BVH arity the kernels traversed (2 or 4) */
   int32_t lds_scene;       /* 1: nodes (and leaf records) ran from the LDS cache */
+  int32_t chunk_samples;   /* samples per work chunk (opts.chunk or the adaptive choice) */
+  int32_t _pad2;
 } rt_stats;
 
 /* Render this rank's rows; out_rgb (host) receives linear mean RGB

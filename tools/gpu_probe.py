@@ -1,7 +1,7 @@
 """Quick GPU timing probe: render a config once and print throughput (dev tool).
 usage: gpu_probe.py scene width spp [modes] [aspect]"""
 import sys, time, json
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 import go_raytracer_amd as rt
 
 scene = sys.argv[1] if len(sys.argv) > 1 else "cornell"

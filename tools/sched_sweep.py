@@ -1,7 +1,7 @@
 """Sweep the fused kernel's scheduling knobs (dev tool):
 python3 tools/sched_sweep.py scene width spp  budget1,budget2 shade1,shade2"""
 import json, os, sys, time
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 import go_raytracer_amd as rt
 
 scene, width, spp = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
