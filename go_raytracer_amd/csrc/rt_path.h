@@ -203,13 +203,17 @@ constexpr uint32_t TRAV_DONE = 0xFFFFFFFFu;  // never a node or leaf code (host_
 struct Trav {
   f3 inv;
   uint32_t cur;
-  int sp;
+  int sp;        // stack depth; entry sp-1 lives in `top`, entries below in TravStack
+  uint32_t top;  // register copy of the top entry: a pop uses it at once and refills it
+                 // from LDS in the background (the refill lands while the popped
+                 // subtree is traversed), taking the LDS latency off the pop
   Hit best;
 };
 RT_D void trav_init(const DevScene& sc, f3 d, Trav& tr) {
   tr.inv = mk3(rcp(d.x), rcp(d.y), rcp(d.z));
   tr.cur = sc.root == PRIM_NONE ? TRAV_DONE : sc.root;
   tr.sp = 0;
+  tr.top = 0;
   tr.best = {kInf, 0.0f, 0.0f, PRIM_NONE};
 }
 
@@ -220,6 +224,20 @@ RT_D void trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const 
                      f3 o, f3 d, float time, float tmin, Trav& tr, int budget) {
   uint32_t cur = tr.cur;
   int sp = tr.sp;
+  uint32_t top = tr.top;
+  // The register top is used with the BVH2 only (tiny LDS scenes, +1.2 % on C2):
+  // with the BVH4 its extra store per push cost C3-C5 1-2 %.
+  constexpr bool kTopReg = !W4;
+  // push v: with kTopReg the old top goes down to the stack proper (entry sp-1)
+  auto push = [&](uint32_t v) {
+    if (kTopReg) {
+      if (sp > 0) stack.push(sp - 1, top);
+      top = v;
+      ++sp;
+    } else {
+      stack.push(sp++, v);
+    }
+  };
   const f3 inv = tr.inv;
   for (int n = 0; n < budget && cur != TRAV_DONE; ++n) {
     if (!W4 && !(cur & LEAF_BIT)) {
@@ -233,7 +251,7 @@ RT_D void trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const 
       const uint32_t c0 = fbits(a0.w), c1 = fbits(a1.w);
       if (h0 && h1) {
         const uint32_t nearc = t0 <= t1 ? c0 : c1, farc = t0 <= t1 ? c1 : c0;
-        if (sp < kStack) stack.push(sp++, farc);
+        if (sp < kStack) push(farc);
         cur = nearc;
         continue;
       }
@@ -280,9 +298,9 @@ RT_D void trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const 
       cx(1, 3);
       cx(1, 2);
       if (tn[0] != kInf) {
-        if (tn[3] != kInf && sp < kStack) stack.push(sp++, ch[3]);
-        if (tn[2] != kInf && sp < kStack) stack.push(sp++, ch[2]);
-        if (tn[1] != kInf && sp < kStack) stack.push(sp++, ch[1]);
+        if (tn[3] != kInf && sp < kStack) push(ch[3]);
+        if (tn[2] != kInf && sp < kStack) push(ch[2]);
+        if (tn[1] != kInf && sp < kStack) push(ch[1]);
         cur = ch[0];
         continue;
       }
@@ -310,10 +328,18 @@ RT_D void trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const 
         }
       }
     }
-    cur = sp == 0 ? TRAV_DONE : stack.pop(--sp);
+    if (sp == 0) {
+      cur = TRAV_DONE;
+    } else if (kTopReg) {
+      cur = top;
+      if (--sp > 0) top = stack.pop(sp - 1);
+    } else {
+      cur = stack.pop(--sp);
+    }
   }
   tr.cur = cur;
   tr.sp = sp;
+  tr.top = top;
 }
 
 // the whole traversal at once (wavefront extend kernel)
