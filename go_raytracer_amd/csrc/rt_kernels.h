@@ -124,6 +124,32 @@ RT_D bool hit_sphere_d(const DevScene& sc, uint32_t i, f3 o, f3 d, float time, d
   t_out = root;
   return true;
 }
+// Both roots of the sphere quadratic, as hit_sphere_d computes them (same
+// arithmetic, so identical doubles): r0 <= r1.  False when the ray misses.
+RT_D bool sphere_roots_d(const DevScene& sc, uint32_t i, f3 o, f3 d, float time, double& r0,
+                         double& r1) {
+  const F4 cr = sc.sph_cr[i];
+  const F4 mv = sc.sph_mv[i];
+  double cx = (double)cr.x + (double)time * (double)mv.x;
+  double cy = (double)cr.y + (double)time * (double)mv.y;
+  double cz = (double)cr.z + (double)time * (double)mv.z;
+  double ox = cx - (double)o.x, oy = cy - (double)o.y, oz = cz - (double)o.z;
+  double dx = d.x, dy = d.y, dz = d.z;
+  double a = dx * dx + dy * dy + dz * dz;
+  double h = dx * ox + dy * oy + dz * oz;
+  double r = cr.w;
+  double c = ox * ox + oy * oy + oz * oz - r * r;
+  double disc = h * h - a * c;
+  if (disc < 0) return false;
+  double sq = __builtin_amdgcn_sqrt(disc);
+  sq = disc > 0.0 ? fma(0.5 * fma(-sq, sq, disc), __builtin_amdgcn_rcp(sq), sq) : 0.0;
+  double ia = __builtin_amdgcn_rcp(a);
+  ia = fma(ia, fma(-a, ia, 1.0), ia);
+  r0 = (h - sq) * ia;
+  r1 = (h + sq) * ia;
+  return true;
+}
+
 RT_D bool hit_sphere(const DevScene& sc, uint32_t i, f3 o, f3 d, float time, float tmin,
                      float tmax, float& t_out) {
   double t;

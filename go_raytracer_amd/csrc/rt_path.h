@@ -380,8 +380,20 @@ RT_D void trace_media(const Params& P, f3 o, f3 d, float time, float tmin, uint3
   for (int mi = 0; mi < sc.n_media; ++mi) {
     const DevMedium m = sc.media[mi];
     double t1, t2;
-    if (!boundary_hit(sc, m, o, d, time, -(double)kInf, (double)kInf, t1)) continue;
-    if (!boundary_hit(sc, m, o, d, time, t1 + 0.0001, (double)kInf, t2)) continue;
+    const uint32_t b0 = m.bcount == 1 ? sc.medium_refs[m.bfirst] : PRIM_NONE;
+    if ((b0 >> 30) == PRIM_SPHERE && b0 != PRIM_NONE) {
+      // a sphere boundary (book2's fog and glass-ball interior): one quadratic gives
+      // both boundary.Hit calls of medium.go:33-42 — t1 = the smaller root (always
+      // inside (-inf, inf)), t2 = the larger one if it exceeds t1 + 1e-4
+      double r0, r1;
+      if (!sphere_roots_d(sc, b0 & 0x3FFFFFFFu, o, d, time, r0, r1)) continue;
+      t1 = r0;
+      if (!(t1 + 0.0001 < r1 && r1 < (double)kInf)) continue;
+      t2 = r1;
+    } else {
+      if (!boundary_hit(sc, m, o, d, time, -(double)kInf, (double)kInf, t1)) continue;
+      if (!boundary_hit(sc, m, o, d, time, t1 + 0.0001, (double)kInf, t2)) continue;
+    }
     t1 = fmax(t1, (double)tmin);
     if (t1 >= t2) continue;
     t1 = fmax(0.0, t1);
