@@ -10,9 +10,10 @@ namespace rt {
 
 constexpr int kLdsNodes = 384;   // 64-B slots staged in LDS per workgroup (24 KB): BVH nodes,
                                  // then the leaf records when both fit (LDS instantiation)
-constexpr int kLdsWMax = 4;      // clamp-weight stack entries per lane kept in LDS (fused, max)
+constexpr int kLdsWMax = 6;      // clamp-weight stack entries per lane kept in LDS (fused, max)
 constexpr int kStack = 64;       // traversal stack entries per lane (LDS short stack + HBM overflow)
 constexpr int kShortStack = 12;  // LDS entries per lane (column layout: [entry][thread])
+constexpr int kShortStackMin = 6;  // smallest short stack of any kernel (fused lean set)
 constexpr int kMaxIt = 1 << 16;  // per-iteration counter slots (no per-iteration memsets)
 constexpr int kXcd = 8;          // queue counters are sharded per XCD (blockIdx % 8)
 
@@ -69,7 +70,7 @@ struct Params {
   Counters* ctr;
   unsigned long long* accum;  // 3 planes x npix, fixed point 2^-32
   uint32_t* pflags;           // per pixel NaN (bits 0-2) / Inf (bits 3-5)
-  uint32_t* ostack;            // traversal-stack overflow [kStack - kShortStack][stack_cols]
+  uint32_t* ostack;            // traversal-stack overflow [kStack - kShortStackMin][stack_cols]
   uint32_t stack_cols;         // = launched threads of the traversal kernel
   F4* trace;                  // debug path trace (3 F4 per vertex) or null
   uint32_t trace_gpix, trace_sample;
@@ -154,6 +155,7 @@ RT_D void slab(const F4& lo, const F4& hi, f3 o, f3 inv, float tmin, float tmax,
 // Explicit address spaces: with generic pointers hipcc selects between the two
 // bases and emits a flat load (slower, counts against both vmcnt and lgkmcnt).
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) float lds_f32;
 typedef __attribute__((address_space(1))) uint32_t glb_u32;
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4f lds_v4;
@@ -178,16 +180,17 @@ struct TravStack {
   uint32_t* lds;     // &lds_stack[0][threadIdx.x], stride blockDim.x
   uint32_t* ovf;     // &ostack[slot], stride cols
   uint32_t cols;
+  int nshort;        // LDS entries (a compile-time constant of each kernel)
   RT_D void push(int sp, uint32_t v) const {
-    if (sp < kShortStack) ((lds_u32*)lds)[sp * 256] = v;
-    else ((glb_u32*)ovf)[(size_t)(sp - kShortStack) * cols] = v;
+    if (sp < nshort) ((lds_u32*)lds)[sp * 256] = v;
+    else ((glb_u32*)ovf)[(size_t)(sp - nshort) * cols] = v;
   }
   RT_D uint32_t pop(int sp) const {
     uint32_t v;
-    if (sp < kShortStack) {
+    if (sp < nshort) {
       v = ((lds_u32*)lds)[sp * 256];
     } else {
-      v = ((glb_u32*)ovf)[(size_t)(sp - kShortStack) * cols];
+      v = ((glb_u32*)ovf)[(size_t)(sp - nshort) * cols];
       wait_vm();
     }
     return v;
@@ -648,11 +651,17 @@ RT_D void set_acc(const Params& P, uint32_t slot, Path& s, f3 v) {
 // shallow pushes off the vector-memory counter (a store holds vmcnt for
 // hundreds of cycles and every later load waits behind it).
 struct WStack {
-  F4* lds;  // &lds_w[0][threadIdx.x], stride 256
+  float* lds;  // &lds_w[0][0][threadIdx.x]: [channel][entry][thread] planes, 12 B per entry
   int nlds;
   RT_D void put(const Params& P, uint32_t slot, uint32_t k, F4 v) const {
-    if ((int)k < nlds) st_lds(lds + k * 256, v);
-    else st_glb(P.stack + (size_t)(k - nlds) * P.P + slot, v);
+    if ((int)k < nlds) {
+      lds_f32* q = (lds_f32*)lds + k * 256;
+      q[0] = v.x;
+      q[nlds * 256] = v.y;
+      q[2 * nlds * 256] = v.z;
+    } else {
+      st_glb(P.stack + (size_t)(k - nlds) * P.P + slot, v);
+    }
   }
   // backward clamp fold over entries nst-1 .. 0 (camera.go:328-330): the HBM
   // entries (rare) one by one, the LDS entries read together and applied unrolled
@@ -660,25 +669,17 @@ struct WStack {
     for (int k = (int)nst - 1; k >= nlds; --k)
       L = clamp_contribution(xyz(ld_glb(P.stack + (size_t)(k - nlds) * P.P + slot)) * L, P.maxc);
     if (nlds > 0 && nst > 0) {
-      F4 e[kLdsWMax];
+      const lds_f32* q = (const lds_f32*)lds;
+      f3 e[kLdsWMax];
 #pragma unroll
       for (int i = 0; i < kLdsWMax; ++i)
-        if (i < nlds) e[i] = ld_lds(lds + i * 256);  // entries >= nst are garbage, unused
+        if (i < nlds)  // entries >= nst are garbage, unused
+          e[i] = mk3(q[i * 256], q[(nlds + i) * 256], q[(2 * nlds + i) * 256]);
 #pragma unroll
       for (int i = kLdsWMax - 1; i >= 0; --i)
-        if (i < nlds && i < (int)nst) L = clamp_contribution(xyz(e[i]) * L, P.maxc);
+        if (i < nlds && i < (int)nst) L = clamp_contribution(e[i] * L, P.maxc);
     }
     return L;
-  }
-  RT_D F4 get(const Params& P, uint32_t slot, uint32_t k) const {
-    F4 v;
-    if ((int)k < nlds) {
-      v = ld_lds(lds + k * 256);
-    } else {
-      v = ld_glb(P.stack + (size_t)(k - nlds) * P.P + slot);
-      if (nlds > 0) wait_vm();
-    }
-    return v;
   }
 };
 

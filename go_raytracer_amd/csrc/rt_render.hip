@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) void k_extend(Params P, int it) {
   __shared__ uint32_t lstack[kShortStack * 256];
   const bool recs_lds = LDS && stage_nodes(P, lnodes, 8);
   const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
-  const TravStack ts = {&lstack[threadIdx.x], P.ostack + gtid, P.stack_cols};
+  const TravStack ts = {&lstack[threadIdx.x], P.ostack + gtid, P.stack_cols, kShortStack};
   const uint32_t sel = (uint32_t)it & 1u;
   uint32_t cnt[kXcd];
   uint32_t n = 0;
@@ -173,18 +173,25 @@ constexpr int fused_waves(uint32_t ft) {
 }
 // LDS weight-stack entries: 3 for the 6-wave lean kernel (its LDS budget), 4 elsewhere
 // (book2's longer paths: 3 entries cost it 5 %)
-constexpr int fused_wlds(uint32_t ft) { return ft == 0u ? 3 : 4; }
+// LDS clamp-weight entries (12 B each): 6 (C2 +1 %, C3 +2.5 % over 3-4), 4 for the
+// mesh set, whose specular paths rarely push weights (C5 -1.5 % with 6)
+constexpr int fused_wlds(uint32_t ft) {
+  return ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? 4 : kLdsWMax;
+}
+// short traversal stack: 6 entries for the lean set (its scenes are tiny trees;
+// the LDS is needed for 6 waves/SIMD), 12 elsewhere; deeper entries go to HBM
+constexpr int fused_short(uint32_t ft) { return ft == 0u ? kShortStackMin : kShortStack; }
 constexpr unsigned fused_static_lds(uint32_t ft) {
-  return (unsigned)(kShortStack * 4 + fused_wlds(ft) * 16) * 256u;
+  return (unsigned)(fused_short(ft) * 4 + fused_wlds(ft) * 12) * 256u;
 }
 template <bool LDS, uint32_t FT, bool W4>
 __global__ __launch_bounds__(256, fused_waves(FT)) void k_fused(Params P) {
   extern __shared__ F4 lnodes[];  // LDS scene cache, sized at launch (scene_lds_bytes)
-  __shared__ uint32_t lstack[kShortStack * 256];
-  __shared__ F4 lw[fused_wlds(FT) * 256];
+  __shared__ uint32_t lstack[fused_short(FT) * 256];
+  __shared__ float lw[3 * fused_wlds(FT) * 256];
   const bool recs_lds = LDS && stage_nodes(P, lnodes, W4 ? 8 : 4);
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;  // weight-stack column
-  const TravStack ts = {&lstack[threadIdx.x], P.ostack + slot, P.stack_cols};
+  const TravStack ts = {&lstack[threadIdx.x], P.ostack + slot, P.stack_cols, fused_short(FT)};
   const WStack ws = {&lw[threadIdx.x], fused_wlds(FT)};
   Path s;
   s.segs = 0;
@@ -635,7 +642,7 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
         st->allocs.erase(std::find(st->allocs.begin(), st->allocs.end(), (void*)st->ostack));
         st->ostack = nullptr;
       }
-      if ((rc = dalloc(st, &st->ostack, (size_t)(kStack - kShortStack) * cols))) return rc;
+      if ((rc = dalloc(st, &st->ostack, (size_t)(kStack - kShortStackMin) * cols))) return rc;
       st->ostack_cols = cols;
     }
   }
