@@ -184,12 +184,13 @@ constexpr int fused_short(uint32_t ft) { return ft == 0u ? kShortStackMin : kSho
 constexpr unsigned fused_static_lds(uint32_t ft) {
   return (unsigned)(fused_short(ft) * 4 + fused_wlds(ft) * 12) * 256u;
 }
-template <bool LDS, uint32_t FT, bool W4>
+// TREE: 4 = BVH4, 2 = BVH2, 0 = no tree (every record tested, tiny scenes)
+template <bool LDS, uint32_t FT, int TREE>
 __global__ __launch_bounds__(256, fused_waves(FT)) void k_fused(Params P) {
   extern __shared__ F4 lnodes[];  // LDS scene cache, sized at launch (scene_lds_bytes)
   __shared__ uint32_t lstack[fused_short(FT) * 256];
   __shared__ float lw[3 * fused_wlds(FT) * 256];
-  const bool recs_lds = LDS && stage_nodes(P, lnodes, W4 ? 8 : 4);
+  const bool recs_lds = LDS && stage_nodes(P, lnodes, TREE == 4 ? 8 : 4);
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;  // weight-stack column
   const TravStack ts = {&lstack[threadIdx.x], P.ostack + slot, P.stack_cols, fused_short(FT)};
   const WStack ws = {&lw[threadIdx.x], fused_wlds(FT)};
@@ -213,8 +214,13 @@ __global__ __launch_bounds__(256, fused_waves(FT)) void k_fused(Params P) {
     }
     if (!__any(has)) break;
     if (has && tr.cur != TRAV_DONE)
-      trav_steps<LDS, FT, W4>(P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, tr,
-                              P.step_budget);
+    {
+      if (TREE == 0)
+        trav_brute<FT>(P.sc, lnodes, s.o, s.d, s.time, 0.001f, tr);
+      else
+        trav_steps<LDS, FT, TREE == 4>(P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, tr,
+                                       P.step_budget);
+    }
     const bool ready = has && tr.cur == TRAV_DONE;
     const uint32_t n_ready = (uint32_t)__popcll(__ballot(ready));
     const bool busy = __any(has && !ready);
@@ -517,10 +523,10 @@ static_assert(FT_SPHERE == RT_FT_SPHERE && FT_TRI == RT_FT_TRI && FT_METAL == RT
 template <bool LDS>
 static const void* fused_for(uint32_t set) {
   switch (set) {
-    case kFtSets[0]: return (const void*)k_fused<LDS, kFtSets[0], true>;
-    case kFtSets[1]: return (const void*)k_fused<LDS, kFtSets[1], true>;
-    case kFtSets[2]: return (const void*)k_fused<LDS, kFtSets[2], true>;
-    default: return (const void*)k_fused<LDS, FT_ALL, true>;
+    case kFtSets[0]: return (const void*)k_fused<LDS, kFtSets[0], 4>;
+    case kFtSets[1]: return (const void*)k_fused<LDS, kFtSets[1], 4>;
+    case kFtSets[2]: return (const void*)k_fused<LDS, kFtSets[2], 4>;
+    default: return (const void*)k_fused<LDS, FT_ALL, 4>;
   }
 }
 static uint32_t pick_set(uint32_t feats) {
@@ -529,10 +535,12 @@ static uint32_t pick_set(uint32_t feats) {
   return FT_ALL;
 }
 // BVH2 kernels exist for the two smallest sets with the tree in LDS (tiny scenes)
-static const void* pick_fused(bool lds, uint32_t set, bool w4) {
-  if (!w4 && lds && set == kFtSets[0]) return (const void*)k_fused<true, kFtSets[0], false>;
-  if (!w4 && lds && set == kFtSets[1]) return (const void*)k_fused<true, kFtSets[1], false>;
-  if (!w4) return nullptr;  // no such kernel: render_impl never asks (see w4 there)
+static const void* pick_fused(bool lds, uint32_t set, int tree) {
+  if (tree == 0 && lds && set == kFtSets[0]) return (const void*)k_fused<true, kFtSets[0], 0>;
+  if (tree == 0 && lds && set == kFtSets[1]) return (const void*)k_fused<true, kFtSets[1], 0>;
+  if (tree == 2 && lds && set == kFtSets[0]) return (const void*)k_fused<true, kFtSets[0], 2>;
+  if (tree == 2 && lds && set == kFtSets[1]) return (const void*)k_fused<true, kFtSets[1], 2>;
+  if (tree != 4) return nullptr;  // no such kernel: render_impl never asks (see tree there)
   return lds ? fused_for<true>(set) : fused_for<false>(set);
 }
 
@@ -582,14 +590,25 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   const size_t lds_slots = std::min<size_t>(
       kLdsNodes,
       (160u * 1024u / (unsigned)fused_waves(ft_set) - fused_static_lds(ft_set) - 512u) / 64u);
-  const bool w4 = mode == RT_MODE_WAVEFRONT || n_refs > 64 || s->h.nodes.empty() ||
-                  (ft_set != kFtSets[0] && ft_set != kFtSets[1]) ||
-                  s->h.nodes.size() / 4 + n_refs > lds_slots;
-  const size_t n_nodes = w4 ? s->h.nodes4.size() / 8 : s->h.nodes.size() / 4;
+  const bool small_set = ft_set == kFtSets[0] || ft_set == kFtSets[1];
+  // tree: 0 (no tree: every record tested, <= kBruteMax records in LDS), 2 or 4
+  const int env_tree = env_int("RT_TREE", -1);
+  int tree = 4;
+  if (mode == RT_MODE_FUSED && small_set && n_refs > 0 && n_refs <= kBruteMax &&
+      n_refs <= lds_slots)
+    tree = 0;
+  else if (mode == RT_MODE_FUSED && small_set && n_refs <= 64 && !s->h.nodes.empty() &&
+           s->h.nodes.size() / 4 + n_refs <= lds_slots)
+    tree = 2;
+  if (mode == RT_MODE_FUSED && small_set && (env_tree == 2 || env_tree == 4) &&
+      (env_tree == 4 || (!s->h.nodes.empty() && s->h.nodes.size() / 4 + n_refs <= lds_slots)))
+    tree = env_tree;  // A/B override
+  const bool w4 = tree == 4;
+  const size_t n_nodes = tree == 4 ? s->h.nodes4.size() / 8 : tree == 2 ? s->h.nodes.size() / 4 : 0;
   const size_t node_slots = w4 ? 2 : 1;  // 64-B LDS slots per node
   const bool f_lds = node_slots * n_nodes <= lds_slots;
   const bool f_recs = f_lds && node_slots * n_nodes + n_refs <= lds_slots;
-  const void* fused_kernel = pick_fused(f_lds, ft_set, w4);
+  const void* fused_kernel = pick_fused(f_lds, ft_set, tree);
   if (!fused_kernel) return set_error(RT_ERR_UNSUPPORTED, "internal: no fused kernel for this scene");
   const size_t fused_lds = f_lds ? 64 * (node_slots * n_nodes + (f_recs ? n_refs : 0)) : 0;
   if (mode == RT_MODE_FUSED) {
@@ -655,10 +674,12 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
 
   Params p{};
   p.sc = s->dev->d;
-  if (!w4) {
+  if (tree == 2) {
     p.sc.nodes = s->dev->nodes2;
     p.sc.root = s->dev->root2;
     p.sc.n_nodes = s->dev->n_nodes2;
+  } else if (tree == 0) {
+    p.sc.n_nodes = 0;  // records only (stage_nodes puts them at the start of the cache)
   }
   for (int i = 0; i < 3; ++i) {
     p.p00r[i] = (float)(cd.pixel00[i] - cd.center[i]);
@@ -829,7 +850,7 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     stats->path_slots = (int32_t)P;
     stats->kernel_features = mode == RT_MODE_FUSED ? (int32_t)ft_set : (int32_t)FT_ALL;
     stats->scene_features = (int32_t)feats;
-    stats->tree_width = w4 ? 4 : 2;
+    stats->tree_width = tree;
     stats->chunk_samples = (int32_t)K;
     stats->lds_scene = mode == RT_MODE_FUSED ? (f_lds ? 1 : 0) : (lds_nodes ? 1 : 0);
     auto sum_ms = [&](const std::vector<std::pair<int, int>>& v, double* acc) -> int {
