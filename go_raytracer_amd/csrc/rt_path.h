@@ -14,7 +14,7 @@ constexpr int kLdsWMax = 6;      // clamp-weight stack entries per lane kept in 
 constexpr int kStack = 64;       // traversal stack entries per lane (LDS short stack + HBM overflow)
 constexpr int kShortStack = 12;  // LDS entries per lane (column layout: [entry][thread])
 constexpr int kShortStackMin = 6;  // smallest short stack of any kernel (fused lean set)
-constexpr int kBruteMax = 32;      // scenes up to this many leaf entries skip the tree (fused)
+constexpr int kBruteMax = 48;      // scenes up to this many leaf entries skip the tree (fused)
 constexpr int kMaxIt = 1 << 16;  // per-iteration counter slots (no per-iteration memsets)
 constexpr int kXcd = 8;          // queue counters are sharded per XCD (blockIdx % 8)
 
@@ -350,13 +350,24 @@ RT_D void trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const 
 // the same record at the same time (a broadcast ds_read, no divergence, no stack),
 // which on 64-wide SIMDs beats a divergent BVH walk when the scene has a few dozen
 // prims (C2: 18 quads).  Closest hit over all records = BVHNode.Hit's result.
-template <uint32_t FT>
+template <uint32_t FT, bool SMEM>
 RT_D void trav_brute(const DevScene& sc, const F4* lrec, f3 o, f3 d, float time, float tmin,
                      Trav& tr) {
   const int n = sc.n_refs;
   for (int k = 0; k < n; ++k) {
-    const F4* q = lrec + 4 * k;
-    const F4 rec[4] = {ld_lds(q), ld_lds(q + 1), ld_lds(q + 2), ld_lds(q + 3)};
+    F4 rec[4];
+    if (SMEM) {  // wave-uniform address: scalar loads into SGPRs (no LDS, no VMEM)
+      typedef __attribute__((address_space(4))) const v4f cst_v4;
+      const cst_v4* q = (const cst_v4*)sc.leafprims + 4 * __builtin_amdgcn_readfirstlane(k);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const v4f v = q[e];
+        rec[e] = {v.x, v.y, v.z, v.w};
+      }
+    } else {
+      const F4* q = lrec + 4 * k;
+      rec[0] = ld_lds(q), rec[1] = ld_lds(q + 1), rec[2] = ld_lds(q + 2), rec[3] = ld_lds(q + 3);
+    }
     float t, u, v;
     uint32_t ref;
     if (hit_record<FT>(rec, o, d, time, tmin, tr.best.t, t, u, v, ref)) {

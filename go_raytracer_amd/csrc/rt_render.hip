@@ -216,7 +216,7 @@ __global__ __launch_bounds__(256, fused_waves(FT)) void k_fused(Params P) {
     if (has && tr.cur != TRAV_DONE)
     {
       if (TREE == 0)
-        trav_brute<FT>(P.sc, lnodes, s.o, s.d, s.time, 0.001f, tr);
+        trav_brute<FT, !LDS>(P.sc, lnodes, s.o, s.d, s.time, 0.001f, tr);
       else
         trav_steps<LDS, FT, TREE == 4>(P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, tr,
                                        P.step_budget);
@@ -538,6 +538,8 @@ static uint32_t pick_set(uint32_t feats) {
 static const void* pick_fused(bool lds, uint32_t set, int tree) {
   if (tree == 0 && lds && set == kFtSets[0]) return (const void*)k_fused<true, kFtSets[0], 0>;
   if (tree == 0 && lds && set == kFtSets[1]) return (const void*)k_fused<true, kFtSets[1], 0>;
+  if (tree == 0 && !lds && set == kFtSets[0]) return (const void*)k_fused<false, kFtSets[0], 0>;
+  if (tree == 0 && !lds && set == kFtSets[1]) return (const void*)k_fused<false, kFtSets[1], 0>;
   if (tree == 2 && lds && set == kFtSets[0]) return (const void*)k_fused<true, kFtSets[0], 2>;
   if (tree == 2 && lds && set == kFtSets[1]) return (const void*)k_fused<true, kFtSets[1], 2>;
   if (tree != 4) return nullptr;  // no such kernel: render_impl never asks (see tree there)
@@ -594,8 +596,12 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   // tree: 0 (no tree: every record tested, <= kBruteMax records in LDS), 2 or 4
   const int env_tree = env_int("RT_TREE", -1);
   int tree = 4;
-  if (mode == RT_MODE_FUSED && small_set && n_refs > 0 && n_refs <= kBruteMax &&
-      n_refs <= lds_slots)
+  const size_t brute_max = (size_t)env_int("RT_BRUTE_MAX", kBruteMax);  // A/B override
+  // Record loop vs tree, measured on the Cornell box plus 0-12 extra boxes
+  // (tools/brute_sweep.py, profiles/r1_brute_sweep.jsonl): the lockstep loop wins
+  // up to ~56 records (18: +33 %, 48: +16 %), reading the records from the LDS
+  // cache when they fit (C2 +2 % over scalar loads), with scalar loads otherwise.
+  if (mode == RT_MODE_FUSED && small_set && n_refs > 0 && n_refs <= brute_max)
     tree = 0;
   else if (mode == RT_MODE_FUSED && small_set && n_refs <= 64 && !s->h.nodes.empty() &&
            s->h.nodes.size() / 4 + n_refs <= lds_slots)
@@ -603,10 +609,13 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   if (mode == RT_MODE_FUSED && small_set && (env_tree == 2 || env_tree == 4) &&
       (env_tree == 4 || (!s->h.nodes.empty() && s->h.nodes.size() / 4 + n_refs <= lds_slots)))
     tree = env_tree;  // A/B override
+  const int smem_env = env_int("RT_BRUTE_SMEM", -1);
+  const bool brute_smem =
+      tree == 0 && (smem_env >= 0 ? smem_env != 0 : n_refs > lds_slots);
   const bool w4 = tree == 4;
   const size_t n_nodes = tree == 4 ? s->h.nodes4.size() / 8 : tree == 2 ? s->h.nodes.size() / 4 : 0;
   const size_t node_slots = w4 ? 2 : 1;  // 64-B LDS slots per node
-  const bool f_lds = node_slots * n_nodes <= lds_slots;
+  const bool f_lds = node_slots * n_nodes <= lds_slots && !brute_smem;
   const bool f_recs = f_lds && node_slots * n_nodes + n_refs <= lds_slots;
   const void* fused_kernel = pick_fused(f_lds, ft_set, tree);
   if (!fused_kernel) return set_error(RT_ERR_UNSUPPORTED, "internal: no fused kernel for this scene");

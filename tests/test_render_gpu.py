@@ -76,7 +76,7 @@ def test_full_size_parity_on_row_subsample(rt, oracle, gpu, name, width, spp, as
 # scene's, C2 runs the lean set on its binary tree from LDS, large scenes the BVH4
 @pytest.mark.parametrize("name,width,lean,width_tree,lds", [
     ("cornell", 64, True, 0, 1), ("book1", 64, False, 4, None), ("book2", 64, False, 4, 0),
-    ("model:256x32", 64, False, 4, 0), ("cornell_smoke", 64, False, None, 1)])
+    ("model:256x32", 64, False, 4, 0), ("cornell_smoke", 64, False, 0, 1)])
 def test_kernel_selection(rt, gpu, name, width, lean, width_tree, lds):
     t, cam, w, l = _scene(rt, name, width, 4)
     with rt.Scene(t, w, l) as sc:
