@@ -168,31 +168,39 @@ __global__ __launch_bounds__(256) void k_init(Params P) {
 // FT = compiled-in scene features (rt_device.h), chosen per scene by pick_fused.
 // Waves per SIMD by feature set: the lean sets fit more waves in the register
 // file (VGPRs <= 512 / waves) and in LDS (24 KB static + the scene cache).
-constexpr int fused_waves(uint32_t ft) {
-  return ft == 0u ? 6 : ft == FT_MEDIA ? 4 : ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? 4 : 3;
+#ifndef BRUTE_WAVES
+#define BRUTE_WAVES 6
+#endif
+// The record-loop kernels (TREE 0) need no traversal stack: kBruteWaves.
+constexpr int kBruteWaves = BRUTE_WAVES;
+constexpr int fused_waves(uint32_t ft, int tree = 4) {
+  return (tree == 0 && ft == 0u) ? kBruteWaves  // 7 measured within noise of 6, 8 -3 %
+         : ft == 0u ? 6
+         : ft == FT_MEDIA ? 4
+         : ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? 4 : 3;
 }
-// LDS weight-stack entries: 3 for the 6-wave lean kernel (its LDS budget), 4 elsewhere
-// (book2's longer paths: 3 entries cost it 5 %)
 // LDS clamp-weight entries (12 B each): 6 (C2 +1 %, C3 +2.5 % over 3-4), 4 for the
 // mesh set, whose specular paths rarely push weights (C5 -1.5 % with 6)
 constexpr int fused_wlds(uint32_t ft) {
   return ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? 4 : kLdsWMax;
 }
-// short traversal stack: 6 entries for the lean set (its scenes are tiny trees;
-// the LDS is needed for 6 waves/SIMD), 12 elsewhere; deeper entries go to HBM
-constexpr int fused_short(uint32_t ft) { return ft == 0u ? kShortStackMin : kShortStack; }
-constexpr unsigned fused_static_lds(uint32_t ft) {
-  return (unsigned)(fused_short(ft) * 4 + fused_wlds(ft) * 12) * 256u;
+// short traversal stack: none for the record loop, 6 entries for the lean set
+// (tiny trees; its LDS budget at 6 waves/SIMD), 12 elsewhere; deeper ones in HBM
+constexpr int fused_short(uint32_t ft, int tree = 4) {
+  return tree == 0 ? 0 : ft == 0u ? kShortStackMin : kShortStack;
+}
+constexpr unsigned fused_static_lds(uint32_t ft, int tree = 4) {
+  return (unsigned)(fused_short(ft, tree) * 4 + fused_wlds(ft) * 12) * 256u;
 }
 // TREE: 4 = BVH4, 2 = BVH2, 0 = no tree (every record tested, tiny scenes)
 template <bool LDS, uint32_t FT, int TREE>
-__global__ __launch_bounds__(256, fused_waves(FT)) void k_fused(Params P) {
+__global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) {
   extern __shared__ F4 lnodes[];  // LDS scene cache, sized at launch (scene_lds_bytes)
-  __shared__ uint32_t lstack[fused_short(FT) * 256];
+  __shared__ uint32_t lstack[(fused_short(FT, TREE) > 0 ? fused_short(FT, TREE) : 1) * 256];
   __shared__ float lw[3 * fused_wlds(FT) * 256];
   const bool recs_lds = LDS && stage_nodes(P, lnodes, TREE == 4 ? 8 : 4);
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;  // weight-stack column
-  const TravStack ts = {&lstack[threadIdx.x], P.ostack + slot, P.stack_cols, fused_short(FT)};
+  const TravStack ts = {&lstack[threadIdx.x], P.ostack + slot, P.stack_cols, fused_short(FT, TREE)};
   const WStack ws = {&lw[threadIdx.x], fused_wlds(FT)};
   Path s;
   s.segs = 0;
@@ -589,9 +597,10 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   // BVH2 kernels exist only for the two smallest feature sets with the tree and
   // its records in LDS (pick_fused): anything else takes the BVH4.
   const size_t n_refs = s->h.refs.size();
-  const size_t lds_slots = std::min<size_t>(
-      kLdsNodes,
-      (160u * 1024u / (unsigned)fused_waves(ft_set) - fused_static_lds(ft_set) - 512u) / 64u);
+  auto slots_for = [&](int tr) {
+    return std::min<size_t>(kLdsNodes, (160u * 1024u / (unsigned)fused_waves(ft_set, tr) -
+                                        fused_static_lds(ft_set, tr) - 512u) / 64u);
+  };
   const bool small_set = ft_set == kFtSets[0] || ft_set == kFtSets[1];
   // tree: 0 (no tree: every record tested, <= kBruteMax records in LDS), 2 or 4
   const int env_tree = env_int("RT_TREE", -1);
@@ -604,11 +613,12 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   if (mode == RT_MODE_FUSED && small_set && n_refs > 0 && n_refs <= brute_max)
     tree = 0;
   else if (mode == RT_MODE_FUSED && small_set && n_refs <= 64 && !s->h.nodes.empty() &&
-           s->h.nodes.size() / 4 + n_refs <= lds_slots)
+           s->h.nodes.size() / 4 + n_refs <= slots_for(2))
     tree = 2;
   if (mode == RT_MODE_FUSED && small_set && (env_tree == 2 || env_tree == 4) &&
-      (env_tree == 4 || (!s->h.nodes.empty() && s->h.nodes.size() / 4 + n_refs <= lds_slots)))
+      (env_tree == 4 || (!s->h.nodes.empty() && s->h.nodes.size() / 4 + n_refs <= slots_for(2))))
     tree = env_tree;  // A/B override
+  const size_t lds_slots = slots_for(tree);
   const int smem_env = env_int("RT_BRUTE_SMEM", -1);
   const bool brute_smem =
       tree == 0 && (smem_env >= 0 ? smem_env != 0 : n_refs > lds_slots);
