@@ -285,6 +285,7 @@ struct DeviceScene {
   std::vector<void*> allocs;
   DevScene d{};                 // nodes = BVH4
   const F4* nodes2 = nullptr;   // BVH2 of the same leaves (tiny scenes)
+  const F4* brute_recs = nullptr;  // the leaf records, largest prim first (record loop)
   uint32_t root2 = PRIM_NONE;
   int32_t n_nodes2 = 0;
   ~DeviceScene() {
@@ -450,6 +451,23 @@ static int ensure_scene(Scene* s, int device) {
     UP(recs, leafprims);
     build_light_records(h, lrecs);
     UP(lrecs, light_recs);
+    // record-loop order: largest surface first, so the closest hit tends to be found
+    // early and later records fail the interval test before their slower half
+    std::vector<size_t> ord(h.refs.size());
+    for (size_t i = 0; i < ord.size(); ++i) ord[i] = i;
+    auto area = [&](uint32_t ref) -> double {
+      const uint32_t type = ref >> 30, idx = ref & 0x3FFFFFFFu;
+      if (type == PRIM_QUAD) return h.quad[5 * (size_t)idx + 1].w;
+      if (type == PRIM_TRI) return h.tri[3 * (size_t)idx + 1].w;
+      const double r = h.sph_cr[idx].w;
+      return 4.0 * 3.141592653589793 * r * r;
+    };
+    std::stable_sort(ord.begin(), ord.end(),
+                     [&](size_t a, size_t b) { return area(h.refs[a]) > area(h.refs[b]); });
+    std::vector<F4> brecs(recs.size());
+    for (size_t i = 0; i < ord.size(); ++i)
+      for (int e = 0; e < 4; ++e) brecs[4 * i + e] = recs[4 * ord[i] + e];
+    if ((rc = upload(s->dev, brecs, &s->dev->brute_recs)) != RT_OK) return rc;
   }
   UP(h.media, media);
   UP(h.medium_refs, medium_refs);
@@ -699,6 +717,7 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     p.sc.n_nodes = s->dev->n_nodes2;
   } else if (tree == 0) {
     p.sc.n_nodes = 0;  // records only (stage_nodes puts them at the start of the cache)
+    if (env_int("RT_BRUTE_SORT", 1)) p.sc.leafprims = s->dev->brute_recs;
   }
   for (int i = 0; i < 3; ++i) {
     p.p00r[i] = (float)(cd.pixel00[i] - cd.center[i]);
