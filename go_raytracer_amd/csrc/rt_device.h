@@ -121,7 +121,8 @@ struct DevScene {
   int32_t n_media;
   int32_t medium_draws;
   const DevLight* lights;
-  const F4* light_recs;  // 4 F4 per light entry: quad lights as a leaf record, area in [2].w
+  const F4* light_recs;  // 8 F4 per light entry; quad lights: [0..3] the leaf record with the
+                         // area in [2].w (pdf), [4..6] Q, u, v (sampling)
   int32_t n_lights;
   int32_t n_refs;       // leaf entries (records)
   const DevMaterial* mats;

@@ -162,6 +162,13 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4f lds_v4;
 typedef __attribute__((address_space(1))) v4f glb_v4;
 typedef float v2f __attribute__((ext_vector_type(2)));
+// 16 B from a wave-uniform address through the scalar cache (s_load into SGPRs):
+// for tables indexed by a loop counter or a broadcast index
+RT_D F4 ld_cst(const F4* p) {
+  typedef __attribute__((address_space(4))) const v4f cst_v4;
+  const v4f v = *(const cst_v4*)p;
+  return {v.x, v.y, v.z, v.w};
+}
 RT_D F4 ld_lds(const F4* p) {
   const v4f v = *(const lds_v4*)p;
   return {v.x, v.y, v.z, v.w};
@@ -559,9 +566,15 @@ RT_D float prim_pdf(const DevScene& sc, uint32_t ref, int li, f3 origin, f3 dir)
   float t, u, v, area;
   f3 n;
   if (!HAS(FT_TRI) || type == PRIM_QUAD) {
-    // the light's leaf-record copy: 4 loads and the traversal's quad test
-    const F4* lr = sc.light_recs + 4 * (size_t)li;
-    const F4 rec[4] = {lr[0], lr[1], lr[2], lr[3]};
+    // the light's leaf-record copy (uniform index: scalar loads) and the traversal's quad test
+    F4 rec[4];
+    if (FT != FT_ALL) {
+      const F4* lr = sc.light_recs + 8 * (size_t)__builtin_amdgcn_readfirstlane(li);
+      rec[0] = ld_cst(lr), rec[1] = ld_cst(lr + 1), rec[2] = ld_cst(lr + 2), rec[3] = ld_cst(lr + 3);
+    } else {
+      const F4* lr = sc.light_recs + 8 * (size_t)li;
+      rec[0] = lr[0], rec[1] = lr[1], rec[2] = lr[2], rec[3] = lr[3];
+    }
     if (!hit_quad_rec(rec, origin, dir, 0.001f, kInf, t, u, v)) return 0.0f;
     n = xyz(rec[1]);
     area = rec[2].w;
@@ -579,10 +592,12 @@ RT_D float prim_pdf(const DevScene& sc, uint32_t ref, int li, f3 origin, f3 dir)
 template <uint32_t FT>
 RT_D float lights_pdf(const DevScene& sc, f3 origin, f3 dir) {
   float sum = 0.0f;
-  for (int i = 0; i < sc.n_lights; ++i) {
-    const DevLight L = sc.lights[i];
-    if (L.ref == PRIM_NONE) continue;
-    sum += L.weight * prim_pdf<FT>(sc, L.ref, i, origin, dir);
+  for (int i = 0; i < sc.n_lights; ++i) {  // uniform loop: the table entry is a scalar load
+    const F4 e = FT != FT_ALL ? ld_cst((const F4*)sc.lights + __builtin_amdgcn_readfirstlane(i))
+                              : ((const F4*)sc.lights)[i];
+    const uint32_t ref = fbits(e.x);
+    if (ref == PRIM_NONE) continue;
+    sum += e.z * prim_pdf<FT>(sc, ref, i, origin, dir);
   }
   return sum;
 }
@@ -599,7 +614,8 @@ RT_D f3 lights_random(const DevScene& sc, f3 origin, const rt_u32x4& r) {
     if (sc.lights[mid].lo24 <= u24) lo = mid;
     else hi = mid - 1;
   }
-  const uint32_t ref = sc.lights[lo].ref;
+  const uint32_t ref =
+      FT != FT_ALL && sc.n_lights == 1 ? fbits(ld_cst((const F4*)sc.lights).x) : sc.lights[lo].ref;
   if (ref == PRIM_NONE) return mk3(rt_unit_f(r.v[1]), s0, s1);
   uint32_t type = ref >> 30, idx = ref & 0x3FFFFFFFu;
   if (HAS(FT_SPHERE) && type == PRIM_SPHERE) {  // sphere.Random + randomToSphere objects.go:63-80
@@ -612,8 +628,16 @@ RT_D f3 lights_random(const DevScene& sc, f3 origin, const rt_u32x4& r) {
     return onb_transform(b, mk3(cos2pi(s0) * tt, sin2pi(s0) * tt, z));
   }
   if (!HAS(FT_TRI) || type == PRIM_QUAD) {  // quad.Random objects.go:161-165
-    const F4* q = sc.quad + 5 * (size_t)idx;
-    return (xyz(q[0]) + xyz(q[1]) * s0 + xyz(q[2]) * s1) - origin;
+    // the light record's Q, u, v; one light: a uniform index, so scalar loads
+    F4 Q, U, V;
+    if (FT != FT_ALL && sc.n_lights == 1) {
+      const F4* lr = sc.light_recs + 4;
+      Q = ld_cst(lr), U = ld_cst(lr + 1), V = ld_cst(lr + 2);
+    } else {
+      const F4* lr = sc.light_recs + 8 * (size_t)lo + 4;
+      Q = lr[0], U = lr[1], V = lr[2];
+    }
+    return (xyz(Q) + xyz(U) * s0 + xyz(V) * s1) - origin;
   }
   // Triangle.Random objects.go:369-385 (non-uniform barycentrics kept)
   const F4* tr = sc.tri + 3 * (size_t)idx;

@@ -367,12 +367,16 @@ static void build_leaf_records(const HostScene& h, std::vector<F4>& recs) {
 }
 // light table entries: quad lights as leaf records with the area in [2].w (prim_pdf)
 static void build_light_records(const HostScene& h, std::vector<F4>& recs) {
-  recs.assign(4 * std::max<size_t>(h.lights.size(), 1), F4{0, 0, 0, 0});
+  recs.assign(8 * std::max<size_t>(h.lights.size(), 1), F4{0, 0, 0, 0});
   for (size_t i = 0; i < h.lights.size(); ++i) {
     const uint32_t ref = h.lights[i].ref;
     if (ref == PRIM_NONE || (ref >> 30) != PRIM_QUAD) continue;
-    make_record(h, ref, &recs[4 * i]);
-    recs[4 * i + 2].w = h.quad[5 * (size_t)(ref & 0x3FFFFFFFu) + 1].w;  // area
+    make_record(h, ref, &recs[8 * i]);
+    const F4* q = &h.quad[5 * (size_t)(ref & 0x3FFFFFFFu)];  // Q|D, u|area, v|mat, n, w
+    recs[8 * i + 2].w = q[1].w;                                // area
+    recs[8 * i + 4] = q[0];
+    recs[8 * i + 5] = q[1];
+    recs[8 * i + 6] = q[2];
   }
 }
 static void make_record(const HostScene& h, uint32_t ref, F4* r) {
