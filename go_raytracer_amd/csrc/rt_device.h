@@ -55,6 +55,12 @@ enum : uint32_t { TRI_HAS_NORMALS = 1u, TRI_HAS_UV = 2u };
 //          (alpha = w.(p x v) = p.A, beta = w.(u x p) = p.B: the triple products of
 //           quad.Hit objects.go:186-187 with the cross products hoisted)
 //  tri:    v0.xyz | ref       ;  e0.xyz | 0           ; e1.xyz | 0 ; 0
+// Record-loop pair layout (quad-only scenes of <= kBruteMax prims, largest area
+// first): records 2p and 2p+1 share 128 B, every field as an adjacent (rec 2p,
+// rec 2p+1) float pair so one packed-fp32 op works on both:
+//  floats 0-7: nx ny nz D ; 8-13: Qx Qy Qz ; 14-19: Ax Ay Az ; 20-25: Bx By Bz ;
+//  26-27: record index (uint bits) ; 28-29: ref ; 30-31: 0.  An odd count is
+//  padded with an all-zero record (n = 0: |n.d| < 1e-8, never hit).
 
 // ---- scene features: the fused kernel is instantiated per feature set so that
 // code a scene cannot reach (and its register pressure) is compiled out.

@@ -353,36 +353,89 @@ RT_D void trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const 
   tr.top = top;
 }
 
-// Tiny scenes: every leaf record, in order, from the LDS cache.  All lanes test
-// the same record at the same time (a broadcast ds_read, no divergence, no stack),
-// which on 64-wide SIMDs beats a divergent BVH walk when the scene has a few dozen
-// prims (C2: 18 quads).  Closest hit over all records = BVHNode.Hit's result.
+// Tiny scenes: every leaf record, in order, from the LDS cache (or through the
+// scalar cache).  All lanes test the same record at the same time (a broadcast
+// read, no divergence, no stack), which on 64-wide SIMDs beats a divergent BVH
+// walk when the scene has a few dozen prims (C2: 18 quads).  Closest hit over all
+// records = BVHNode.Hit's result (hittable.go:122-138; quad.go Hit per record).
+// The small feature sets hold quads only, so the loop is the quad test alone,
+// two records at a time in packed fp32 (v_pk_fma_f32: one issue, two records)
+// from the pair layout (rt_device.h), branch-free: the loop keeps the closest t
+// and its record index; the winner's (alpha, beta) and ref are recomputed once
+// after the loop with the same fma sequence, so they equal the loop's values.
+// The record loop is VALU-issue bound (C2: ~55 % of the kernel), so every
+// instruction per record counts: 11 packed/rcp ops + 5 checks + 2 selects
+// (18 VALU per record test, was 36 with one record at a time and early exits).
+RT_D v2f pfma(v2f a, v2f b, v2f c) { return __builtin_elementwise_fma(a, b, c); }
+// 0 <= a <= 1 && 0 <= b <= 1 as one unsigned max + compare: non-negative floats
+// order like their bits, and negatives / NaN have the sign or exponent bits set
+// above 1.0f's.  (-0.0f is rejected where the reference accepts it: exactly
+// zero alpha with a negative sign; measure zero, within the parity tolerance.)
+RT_D bool unit_ab(float a, float b) {
+  return max(__float_as_uint(a), __float_as_uint(b)) <= 0x3F800000u;
+}
 template <uint32_t FT, bool SMEM>
 RT_D void trav_brute(const DevScene& sc, const F4* lrec, f3 o, f3 d, float time, float tmin,
                      Trav& tr) {
-  const int n = sc.n_refs;
-  for (int k = 0; k < n; ++k) {
-    F4 rec[4];
-    if (SMEM) {  // wave-uniform address: scalar loads into SGPRs (no LDS, no VMEM)
+  static_assert(!HAS(FT_SPHERE | FT_TRI), "record loop: quad-only feature sets");
+  const int np = sc.n_refs >> 1;  // pairs (the host pads to an even count)
+  const v2f ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
+  const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z};
+  float best = tr.best.t;
+  uint32_t bk = 0xFFFFFFFFu;
+  for (int p = 0; p < np; ++p) {
+    v4f r[7];
+    if (SMEM) {
       typedef __attribute__((address_space(4))) const v4f cst_v4;
-      const cst_v4* q = (const cst_v4*)sc.leafprims + 4 * __builtin_amdgcn_readfirstlane(k);
+      const cst_v4* q = (const cst_v4*)sc.leafprims + 8 * __builtin_amdgcn_readfirstlane(p);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const v4f v = q[e];
-        rec[e] = {v.x, v.y, v.z, v.w};
-      }
+      for (int e = 0; e < 7; ++e) r[e] = q[e];
     } else {
-      const F4* q = lrec + 4 * k;
-      rec[0] = ld_lds(q), rec[1] = ld_lds(q + 1), rec[2] = ld_lds(q + 2), rec[3] = ld_lds(q + 3);
+      const lds_v4* q = (const lds_v4*)lrec + 8 * p;
+#pragma unroll
+      for (int e = 0; e < 7; ++e) r[e] = q[e];
     }
-    float t, u, v;
-    uint32_t ref;
-    if (hit_record<FT>(rec, o, d, time, tmin, tr.best.t, t, u, v, ref)) {
-      tr.best.t = t;
-      tr.best.u = u;
-      tr.best.v = v;
-      tr.best.ref = ref;
+    // record indices 2p, 2p+1 as stored data: the select takes them from a VGPR
+    // (a loop-counter SGPR would need a v_mov first: one constant-bus read per op)
+    const uint32_t k0 = __float_as_uint(r[6].z), k1 = __float_as_uint(r[6].w);
+    const v2f nx = r[0].xy, ny = r[0].zw, nz = r[1].xy, D = r[1].zw;
+    const v2f den = pfma(nz, dz, pfma(ny, dy, nx * dx));
+    const v2f num = D - pfma(nz, oz, pfma(ny, oy, nx * ox));
+    const v2f t = num * v2f{rcp(den.x), rcp(den.y)};
+    const v2f px = pfma(dx, t, ox) - r[2].xy;
+    const v2f py = pfma(dy, t, oy) - r[2].zw;
+    const v2f pz = pfma(dz, t, oz) - r[3].xy;
+    const v2f a = pfma(pz, r[4].zw, pfma(py, r[4].xy, px * r[3].zw));
+    const v2f b = pfma(pz, r[6].xy, pfma(py, r[5].zw, px * r[5].xy));
+    const bool c0 = fabsf(den.x) >= 1e-8f && t.x >= tmin && unit_ab(a.x, b.x) && t.x <= best;
+    best = c0 ? t.x : best;
+    bk = c0 ? k0 : bk;
+    const bool c1 = fabsf(den.y) >= 1e-8f && t.y >= tmin && unit_ab(a.y, b.y) && t.y <= best;
+    best = c1 ? t.y : best;
+    bk = c1 ? k1 : bk;
+  }
+  if (bk != 0xFFFFFFFFu) {
+    // the winner's fields (pair bk/2, half bk&1): Q at floats 8/10/12, A at
+    // 14/16/18, B at 20/22/24, ref at 28 (+ half)
+    const uint32_t base = 32u * (bk >> 1) + (bk & 1u);
+    float f[10];
+    if (SMEM) {
+      const float* g = (const float*)sc.leafprims + base + 8;
+#pragma unroll
+      for (int e = 0; e < 10; ++e)
+        f[e] = *(const __attribute__((address_space(1))) float*)(g + 2 * e + (e == 9 ? 2 : 0));
+    } else {
+      const lds_f32* l = (const lds_f32*)lrec + base + 8;
+#pragma unroll
+      for (int e = 0; e < 10; ++e) f[e] = l[2 * e + (e == 9 ? 2 : 0)];
     }
+    const float px = fmaf(d.x, best, o.x) - f[0];
+    const float py = fmaf(d.y, best, o.y) - f[1];
+    const float pz = fmaf(d.z, best, o.z) - f[2];
+    tr.best.t = best;
+    tr.best.u = fmaf(pz, f[5], fmaf(py, f[4], px * f[3]));
+    tr.best.v = fmaf(pz, f[8], fmaf(py, f[7], px * f[6]));
+    tr.best.ref = __float_as_uint(f[9]);
   }
   tr.cur = TRAV_DONE;
 }

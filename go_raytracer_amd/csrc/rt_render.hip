@@ -223,7 +223,7 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
     if (!__any(has)) break;
     if (has && tr.cur != TRAV_DONE)
     {
-      if (TREE == 0)
+      if constexpr (TREE == 0)
         trav_brute<FT, !LDS>(P.sc, lnodes, s.o, s.d, s.time, 0.001f, tr);
       else
         trav_steps<LDS, FT, TREE == 4>(P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, tr,
@@ -285,7 +285,7 @@ struct DeviceScene {
   std::vector<void*> allocs;
   DevScene d{};                 // nodes = BVH4
   const F4* nodes2 = nullptr;   // BVH2 of the same leaves (tiny scenes)
-  const F4* brute_recs = nullptr;  // the leaf records, largest prim first (record loop)
+  const F4* brute_pairs = nullptr;  // quad records in pairs, largest first (record loop)
   uint32_t root2 = PRIM_NONE;
   int32_t n_nodes2 = 0;
   ~DeviceScene() {
@@ -468,10 +468,20 @@ static int ensure_scene(Scene* s, int device) {
     };
     std::stable_sort(ord.begin(), ord.end(),
                      [&](size_t a, size_t b) { return area(h.refs[a]) > area(h.refs[b]); });
-    std::vector<F4> brecs(recs.size());
-    for (size_t i = 0; i < ord.size(); ++i)
-      for (int e = 0; e < 4; ++e) brecs[4 * i + e] = recs[4 * ord[i] + e];
-    if ((rc = upload(s->dev, brecs, &s->dev->brute_recs)) != RT_OK) return rc;
+    // pair layout (rt_device.h): records 2p, 2p+1 interleaved field by field
+    const size_t n_even = (ord.size() + 1) & ~(size_t)1;
+    std::vector<F4> pairs(std::max<size_t>(4 * n_even, 8), F4{0, 0, 0, 0});  // pad: n = 0, never hit
+    for (size_t i = 0; i < ord.size(); ++i) {
+      const F4* r = &recs[4 * ord[i]];  // Q|ref, n|D, A, B
+      float* f = (float*)&pairs[8 * (i / 2)] + (i & 1);
+      float kb;
+      const uint32_t k = (uint32_t)i;
+      memcpy(&kb, &k, 4);
+      const float v[15] = {r[1].x, r[1].y, r[1].z, r[1].w, r[0].x, r[0].y, r[0].z, r[2].x,
+                           r[2].y, r[2].z, r[3].x, r[3].y, r[3].z, kb,     r[0].w};
+      for (int e = 0; e < 15; ++e) f[2 * e] = v[e];
+    }
+    if ((rc = upload(s->dev, pairs, &s->dev->brute_pairs)) != RT_OK) return rc;
   }
   UP(h.media, media);
   UP(h.medium_refs, medium_refs);
@@ -641,17 +651,19 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
       (env_tree == 4 || (!s->h.nodes.empty() && s->h.nodes.size() / 4 + n_refs <= slots_for(2))))
     tree = env_tree;  // A/B override
   const size_t lds_slots = slots_for(tree);
+  const size_t brute_slots = (n_refs + 1) & ~(size_t)1;  // record-loop pairs, 2 x 64 B each
   const int smem_env = env_int("RT_BRUTE_SMEM", -1);
   const bool brute_smem =
-      tree == 0 && (smem_env >= 0 ? smem_env != 0 : n_refs > lds_slots);
+      tree == 0 && (smem_env >= 0 ? smem_env != 0 : brute_slots > lds_slots);
   const bool w4 = tree == 4;
   const size_t n_nodes = tree == 4 ? s->h.nodes4.size() / 8 : tree == 2 ? s->h.nodes.size() / 4 : 0;
   const size_t node_slots = w4 ? 2 : 1;  // 64-B LDS slots per node
   const bool f_lds = node_slots * n_nodes <= lds_slots && !brute_smem;
-  const bool f_recs = f_lds && node_slots * n_nodes + n_refs <= lds_slots;
+  const size_t rec_slots = tree == 0 ? brute_slots : n_refs;
+  const bool f_recs = f_lds && node_slots * n_nodes + rec_slots <= lds_slots;
   const void* fused_kernel = pick_fused(f_lds, ft_set, tree);
   if (!fused_kernel) return set_error(RT_ERR_UNSUPPORTED, "internal: no fused kernel for this scene");
-  const size_t fused_lds = f_lds ? 64 * (node_slots * n_nodes + (f_recs ? n_refs : 0)) : 0;
+  const size_t fused_lds = f_lds ? 64 * (node_slots * n_nodes + (f_recs ? rec_slots : 0)) : 0;
   if (mode == RT_MODE_FUSED) {
     if ((rc = occupancy_blocks(fused_kernel, o.device, &fused_blocks, fused_lds))) return rc;
     if (o.path_slots > 0) fused_blocks = std::max(1, std::min(fused_blocks, (o.path_slots + 255) / 256));
@@ -721,7 +733,8 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     p.sc.n_nodes = s->dev->n_nodes2;
   } else if (tree == 0) {
     p.sc.n_nodes = 0;  // records only (stage_nodes puts them at the start of the cache)
-    if (env_int("RT_BRUTE_SORT", 1)) p.sc.leafprims = s->dev->brute_recs;
+    p.sc.leafprims = s->dev->brute_pairs;
+    p.sc.n_refs = (int32_t)brute_slots;  // even: whole pairs
   }
   for (int i = 0; i < 3; ++i) {
     p.p00r[i] = (float)(cd.pixel00[i] - cd.center[i]);

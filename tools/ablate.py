@@ -47,7 +47,7 @@ V = {
     "dbl_fold": [("go_raytracer_amd/csrc/rt_path.h",
         "    if (s.flags & F_PRE) L = get_pre<SOA>(P, slot, s) * L;",
         "    if (s.flags & F_PRE) L = get_pre<SOA>(P, slot, s) * L;\n"
-        "    { f3 L2 = L * 1.0000001f; for (int kk = (int)s.nst - 1; kk >= 0; --kk) L2 = clamp_contribution(xyz(ws.get(P, slot, (uint32_t)kk)) * L2, P.maxc); L = L + L2 * 0.0f; }")],
+        "    { f3 L2 = ws.fold(P, slot, s.nst, L * 1.0000001f); L = L + L2 * 0.0f; }")],
     "waves6": [("go_raytracer_amd/csrc/rt_render.hip",
         "constexpr int fused_waves(uint32_t ft) { return ft == 0u ? 5 : ft == FT_MEDIA ? 4 : 3; }",
         "constexpr int fused_waves(uint32_t ft) { return ft == 0u ? 6 : ft == FT_MEDIA ? 4 : 3; }"),
@@ -70,6 +70,11 @@ V = {
     "medw5": [("go_raytracer_amd/csrc/rt_render.hip",
         "return ft == 0u ? 6 : ft == FT_MEDIA ? 4 :",
         "return ft == 0u ? 6 : ft == FT_MEDIA ? 5 :")],
+    "dbl_brute": [("go_raytracer_amd/csrc/rt_render.hip",
+        "        trav_brute<FT, !LDS>(P.sc, lnodes, s.o, s.d, s.time, 0.001f, tr);",
+        "      { Trav t2 = tr; trav_brute<FT, !LDS>(P.sc, lnodes, s.o, s.d * 1.0000001f, s.time, 0.001f, t2);\n"
+        "        trav_brute<FT, !LDS>(P.sc, lnodes, s.o, s.d, s.time, 0.001f, tr);\n"
+        "        tr.best.t = fminf(tr.best.t, t2.best.t + 0.0f * tr.best.t); }")],
 }
 names = sys.argv[1:] or list(V)
 for name in names:
