@@ -18,7 +18,7 @@ from ._lib import (RT_NOISE_MARBLE, RT_NOISE_PERLIN, RT_NOISE_TURBULENT, RtCamer
                    check, lib)
 
 __all__ = ["Tree", "Camera", "Scene", "quantize", "format_ppm", "device_count", "RtError",
-           "demo_scene", "DEMO_SCENES"]
+           "demo_scene", "DEMO_SCENES", "LoadObjOptions", "DefaultLoadOptions"]
 
 DEMO_SCENES = ("book1", "book2", "book3", "simple_light", "quads", "cornell", "cornell_smoke",
                "model")
@@ -151,10 +151,138 @@ class Tree:
     def medium(self, boundary, density, tex):
         return check(lib().rt_constant_medium(self._p, boundary, density, self._tex(tex)))
 
+    # OBJ/MTL loader (objLoader.go:63-538)
+    def LoadObjWithOptions(self, filename, options=None, mtl_text=None, obj_text=None):
+        """LoadObjWithOptions objLoader.go:72: returns (model, lights) node ids —
+        BuildBVH over every triangle and the list of emissive (and, with
+        FindWindows, dielectric) triangles.  ``obj_text``/``mtl_text`` load from
+        memory instead of the files.  Image maps the C loader cannot decode
+        (anything but binary PPM) are decoded here with PIL, when importable."""
+        o = options if options is not None else DefaultLoadOptions()
+        c, keep = o.to_c(self, filename, mtl_text)
+        model, lights, info = C.c_int(-1), C.c_int(-1), _lib.RtObjInfo()
+        if obj_text is None:
+            check(lib().rt_load_obj(self._p, filename.encode(), C.byref(c), C.byref(model),
+                                    C.byref(lights), C.byref(info)))
+        else:
+            ob = obj_text.encode() if isinstance(obj_text, str) else bytes(obj_text)
+            mb = None if mtl_text is None else (
+                mtl_text.encode() if isinstance(mtl_text, str) else bytes(mtl_text))
+            check(lib().rt_load_obj_memory(
+                self._p, ob, len(ob), mb, 0 if mb is None else len(mb),
+                None if filename is None else filename.encode(), C.byref(c), C.byref(model),
+                C.byref(lights), C.byref(info)))
+        del keep
+        self.last_obj_info = info
+        return model.value, lights.value
+
+    def LoadObj(self, filename, mat=-1):
+        """LoadObj objLoader.go:64: default options with DefaultMaterial = mat."""
+        o = DefaultLoadOptions()
+        o.DefaultMaterial = mat
+        return self.LoadObjWithOptions(filename, o)
+
     def view(self):
         v = RtTreeView()
         check(lib().rt_tree_get_view(self._p, C.byref(v)))
         return v
+
+
+class LoadObjOptions:
+    """LoadObjOptions objLoader.go:18-29 (DefaultMaterial: a material id, -1 = nil)."""
+
+    def __init__(self, **kw):
+        self.ScaleFactor = 1.0
+        self.FlipYZ = False
+        self.Debug = True
+        self.IgnoreNormals = False
+        self.Center = True
+        self.FlipFaces = False
+        self.Position = (0.0, 0.0, 0.0)
+        self.DefaultMaterial = -1
+        self.IgnoreMtl = False
+        self.FindWindows = False
+        for k, v in kw.items():
+            if not hasattr(self, k):
+                raise AttributeError(k)
+            setattr(self, k, v)
+
+    def to_c(self, tree, filename, mtl_text=None):
+        c = _lib.RtObjOptions()
+        check(lib().rt_obj_default_options(C.byref(c)))
+        c.scale_factor = float(self.ScaleFactor)
+        c.flip_yz, c.debug = int(bool(self.FlipYZ)), int(bool(self.Debug))
+        c.ignore_normals, c.center = int(bool(self.IgnoreNormals)), int(bool(self.Center))
+        c.flip_faces = int(bool(self.FlipFaces))
+        c.default_material = int(self.DefaultMaterial)
+        c.position = _d3(self.Position)
+        c.ignore_mtl, c.find_windows = int(bool(self.IgnoreMtl)), int(bool(self.FindWindows))
+        keep = []
+        names = [] if self.IgnoreMtl else _mtl_image_names(filename, mtl_text)
+        imgs = []
+        for n in names:
+            rgb = _decode_image(n)
+            if rgb is None:
+                continue
+            keep.append(rgb)
+            imgs.append(_lib.RtObjImage(n.encode(), rgb.ctypes.data, rgb.shape[1], rgb.shape[0]))
+        if imgs:
+            arr = (_lib.RtObjImage * len(imgs))(*imgs)
+            keep.append(arr)
+            c.n_images, c.images = len(imgs), C.cast(arr, C.POINTER(_lib.RtObjImage))
+        return c, keep
+
+
+def DefaultLoadOptions():
+    """DefaultLoadOptions objLoader.go:32-45."""
+    return LoadObjOptions()
+
+
+def _mtl_image_names(filename, mtl_text):
+    """map_Kd / map_Ka names of the MTL an OBJ references (mtlLoader.go:174-184)."""
+    import os
+    text = mtl_text
+    if text is None:
+        if filename is None or not os.path.exists(filename):
+            return []
+        lib_name = None
+        with open(filename, "rb") as f:
+            for raw in f:
+                p = raw.decode("utf-8", "replace").split()
+                if len(p) >= 2 and p[0] == "mtllib":
+                    lib_name = " ".join(p[1:])
+                    break
+        if lib_name is None:
+            return []
+        path = os.path.join(os.path.dirname(filename), lib_name)
+        if not os.path.exists(path):
+            return []
+        with open(path, "rb") as f:
+            text = f.read()
+    if isinstance(text, bytes):
+        text = text.decode("utf-8", "replace")
+    names = []
+    for line in text.splitlines():
+        p = line.split()
+        if len(p) >= 2 and p[0] in ("map_Kd", "map_Ka"):
+            names.append(" ".join(p[1:]))
+    return names
+
+
+def _decode_image(name):
+    """image.Decode of a map file (imageLoader.go:29-46) for formats the C loader
+    does not read; None leaves the file to the C loader (PPM, or its error)."""
+    import os
+    if not os.path.exists(name):
+        return None
+    with open(name, "rb") as f:
+        if f.read(2) == b"P6":
+            return None
+    try:
+        from PIL import Image
+    except ImportError:
+        return None
+    return np.ascontiguousarray(np.asarray(Image.open(name).convert("RGB")), dtype=np.uint8)
 
 
 class Camera:

@@ -100,6 +100,28 @@ class RtTreeView(C.Structure):
     ]
 
 
+class RtObjImage(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("rgb", C.c_void_p), ("w", C.c_int32), ("h", C.c_int32)]
+
+
+class RtObjOptions(C.Structure):  # LoadObjOptions objLoader.go:18-29
+    _fields_ = [
+        ("scale_factor", C.c_double), ("flip_yz", C.c_int32), ("debug", C.c_int32),
+        ("ignore_normals", C.c_int32), ("center", C.c_int32), ("flip_faces", C.c_int32),
+        ("default_material", C.c_int32), ("position", D3), ("ignore_mtl", C.c_int32),
+        ("find_windows", C.c_int32), ("n_images", C.c_int32), ("_pad", C.c_int32),
+        ("images", C.POINTER(RtObjImage)),
+    ]
+
+
+class RtObjInfo(C.Structure):
+    _fields_ = [
+        ("n_vertices", C.c_int64), ("n_normals", C.c_int64), ("n_texcoords", C.c_int64),
+        ("n_triangles", C.c_int64), ("n_lights", C.c_int64), ("n_materials", C.c_int32),
+        ("default_material", C.c_int32), ("bounds_min", D3), ("bounds_max", D3), ("center", D3),
+    ]
+
+
 _P = C.c_void_p
 _I = C.c_int
 _DP = C.POINTER(C.c_double)
@@ -136,6 +158,12 @@ SIGNATURES = {
     "rt_translate": (_I, [_P, _I, D3]),
     "rt_rotate_y": (_I, [_P, _I, C.c_double]),
     "rt_constant_medium": (_I, [_P, _I, C.c_double, _I]),
+    "rt_obj_default_options": (_I, [C.POINTER(RtObjOptions)]),
+    "rt_load_obj": (_I, [_P, C.c_char_p, C.POINTER(RtObjOptions), C.POINTER(_I), C.POINTER(_I),
+                         C.POINTER(RtObjInfo)]),
+    "rt_load_obj_memory": (_I, [_P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_char_p,
+                                C.POINTER(RtObjOptions), C.POINTER(_I), C.POINTER(_I),
+                                C.POINTER(RtObjInfo)]),
     "rt_tree_get_view": (_I, [_P, C.POINTER(RtTreeView)]),
     "rt_camera_derive": (_I, [C.POINTER(RtCamera), C.POINTER(RtCameraDerived)]),
     "rt_scene_create": (_I, [_P, _I, _I, C.POINTER(_P)]),

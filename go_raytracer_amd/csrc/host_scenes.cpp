@@ -6,11 +6,12 @@
 // (rt_tree_seed) in the same order, so a scene is a pure function of its seed.
 //
 // main.go:371-409 (modelExample) needs dragon.obj, which the reference does not
-// ship (.gitignore:5).  "model" substitutes a procedurally generated (2,3)
-// torus-knot tube with smooth vertex normals (~1.05 M triangles), passed through
-// the same LoadObjWithOptions transform (scale, centre, position,
-// objLoader.go:146-265) and the same scene wrapper.  It is labelled as a
-// substitute everywhere it is reported.
+// ship (.gitignore:5).  "model" loads <asset_dir>/dragon.obj through the OBJ
+// loader (host_obj.cpp) when it is there; otherwise it substitutes a
+// procedurally generated (2,3) torus-knot tube with smooth vertex normals
+// (~1.05 M triangles), written as OBJ text and passed through the same
+// LoadObjWithOptions (scale, centre, position, objLoader.go:146-265) and the same
+// scene wrapper.  It is labelled as a substitute everywhere it is reported.
 #include <math.h>
 #include <stdio.h>
 #include <string.h>
@@ -364,10 +365,17 @@ void knot_point(double s, double* p) {
   p[2] = r * sin(P * s) * 0.18;
 }
 
-int substitute_dragon(rt_tree* t, int nu, int nv, int mat, int* model_out) {
+// The substitute as OBJ text ("OBJ units", before LoadObjWithOptions' scale):
+// nu*nv vertices with vertex normals and one quad face per grid cell, which the
+// loader fans into the triangles (a,b,c), (a,c,d) (objLoader.go:396-397).
+std::string substitute_dragon_obj(int nu, int nv) {
   // tube radius / frame by finite differences + parallel transport
   const double a = 0.055;
-  std::vector<double> verts((size_t)nu * nv * 3), norms((size_t)nu * nv * 3);
+  std::string out;
+  out.reserve((size_t)nu * nv * 190);
+  out += "# go_raytracer_amd substitute for dragon.obj: (2,3) torus-knot tube\n";
+  std::vector<double> norms((size_t)nu * nv * 3);
+  char line[256];
   double prev_n[3] = {0, 1, 0};
   for (int i = 0; i < nu; ++i) {
     double s = 2 * M_PI * i / nu, ds = 1e-4;
@@ -390,55 +398,57 @@ int substitute_dragon(rt_tree* t, int nu, int nv, int mat, int* model_out) {
       double rr = a * (1.0 + 0.18 * sin(7 * phi) * sin(23 * s));
       double dir[3];
       for (int k = 0; k < 3; ++k) dir[k] = cos(phi) * N[k] + sin(phi) * B[k];
-      size_t o = 3 * ((size_t)i * nv + j);
-      for (int k = 0; k < 3; ++k) {
-        verts[o + k] = c0[k] + rr * dir[k];
-        norms[o + k] = dir[k];
-      }
+      snprintf(line, sizeof line, "v %.17g %.17g %.17g\n", c0[0] + rr * dir[0],
+               c0[1] + rr * dir[1], c0[2] + rr * dir[2]);
+      out += line;
+      memcpy(&norms[3 * ((size_t)i * nv + j)], dir, sizeof dir);
     }
   }
-  // LoadObjWithOptions transform: scale by ScaleFactor, centre on the bbox
-  // centre, then add Position (objLoader.go:181-265)
-  const double scale = 5.0;
-  double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-  for (size_t v = 0; v < verts.size() / 3; ++v)
-    for (int k = 0; k < 3; ++k) {
-      verts[3 * v + k] *= scale;
-      mn[k] = fmin(mn[k], verts[3 * v + k]);
-      mx[k] = fmax(mx[k], verts[3 * v + k]);
-    }
-  const double pos[3] = {0, 1.8, 0};
-  for (size_t v = 0; v < verts.size() / 3; ++v)
-    for (int k = 0; k < 3; ++k) verts[3 * v + k] += -((mn[k] + mx[k]) / 2) + pos[k];
-  const size_t ntri = (size_t)nu * nv * 2;
-  std::vector<double> tv(ntri * 9), tn(ntri * 9);
-  std::vector<int32_t> mats(ntri, mat);
-  size_t k = 0;
-  auto put = [&](int i, int j, int slot) {
-    size_t o = 3 * ((size_t)(i % nu) * nv + (j % nv));
-    memcpy(&tv[9 * k + 3 * slot], &verts[o], 3 * sizeof(double));
-    memcpy(&tn[9 * k + 3 * slot], &norms[o], 3 * sizeof(double));
-  };
+  for (size_t v = 0; v < norms.size(); v += 3) {
+    snprintf(line, sizeof line, "vn %.17g %.17g %.17g\n", norms[v], norms[v + 1], norms[v + 2]);
+    out += line;
+  }
+  auto id = [&](int i, int j) { return (long)(i % nu) * nv + (j % nv) + 1; };
   for (int i = 0; i < nu; ++i)
     for (int j = 0; j < nv; ++j) {
-      put(i, j, 0), put(i + 1, j, 1), put(i + 1, j + 1, 2), ++k;  // f v1 v2 v3 (fan of a quad face)
-      put(i, j, 0), put(i + 1, j + 1, 1), put(i, j + 1, 2), ++k;
+      long q[4] = {id(i, j), id(i + 1, j), id(i + 1, j + 1), id(i, j + 1)};
+      snprintf(line, sizeof line, "f %ld//%ld %ld//%ld %ld//%ld %ld//%ld\n", q[0], q[0], q[1], q[1],
+               q[2], q[2], q[3], q[3]);
+      out += line;
     }
-  int list = rt_new_triangles(t, (int)ntri, tv.data(), tn.data(), nullptr, mats.data());
-  CHECK(list);
-  *model_out = rt_build_bvh(t, list);  // objLoader.go:512
-  return *model_out < 0 ? *model_out : RT_OK;
+  return out;
 }
 
-int model(rt_tree* t, const char*, rt_camera* c, int* world_out, int* lights_out, int nu, int nv) {
+// modelExample main.go:371-409: LoadObjWithOptions("dragon.obj") with ScaleFactor 5,
+// Center, Position (0, 1.8, 0), a gold Metal default material; the real file is
+// used when asset_dir holds dragon.obj, otherwise the substitute mesh goes
+// through the same loader from memory.
+int model(rt_tree* t, const char* asset_dir, rt_camera* c, int* world_out, int* lights_out,
+          int nu, int nv) {
   int world = rt_new_list(t);
   int ground = sphere(t, {0, -1000, 0}, 1000, solid_lambert(t, .4, .4, .4));
   CHECK(rt_list_add(t, world, ground));
-  int gold = rt_mat_metal(t, 255.0 / 255.0, 215.0 / 255.0, 0, 0.5);
-  int mdl = -1;
-  CHECK(substitute_dragon(t, nu, nv, gold, &mdl));
-  int lights = rt_new_list(t);  // no emissive triangles in the substitute
+  rt_obj_options opt;
+  rt_obj_default_options(&opt);
+  opt.scale_factor = 5;
+  opt.center = 1;
+  opt.position[0] = 0, opt.position[1] = 1.8, opt.position[2] = 0;
+  opt.debug = 0;  // the reference prints its loader diagnostics (Debug = true); silent here
+  opt.default_material = rt_mat_metal(t, 255.0 / 255.0, 215.0 / 255.0, 0, 0.5);
+  CHECK(opt.default_material);
+  int mdl = -1, lights = -1;
+  std::string path = std::string(asset_dir ? asset_dir : "assets") + "/dragon.obj";
+  FILE* f = nu < 0 ? fopen(path.c_str(), "rb") : nullptr;
+  if (f) {
+    fclose(f);
+    CHECK(rt_load_obj(t, path.c_str(), &opt, &mdl, &lights, nullptr));
+  } else {
+    std::string obj = substitute_dragon_obj(nu < 0 ? 2048 : nu, nv < 0 ? 256 : nv);
+    CHECK(rt_load_obj_memory(t, obj.data(), obj.size(), nullptr, 0, "dragon.obj", &opt, &mdl,
+                             &lights, nullptr));
+  }
   CHECK(rt_list_add(t, world, rt_rotate_y(t, mdl, 180)));
+  // the sun joins the model's light list (main.go:385-391)
   int light = sphere(t, {7, 13, 7}, 5, solid_light(t, 4, 4, 4));
   CHECK(rt_list_add(t, world, light));
   CHECK(rt_list_add(t, lights, light));
@@ -483,7 +493,7 @@ int rt_demo_scene(rt_tree* t, const char* name, const char* asset_dir, rt_camera
   if (n == "quads") return quads(t, asset_dir, cam, world, lights);
   if (n == "cornell") return cornell(t, asset_dir, cam, world, lights);
   if (n == "cornell_smoke") return cornell_smoke(t, asset_dir, cam, world, lights);
-  if (n == "model") return model(t, asset_dir, cam, world, lights, 2048, 256);
+  if (n == "model") return model(t, asset_dir, cam, world, lights, -1, -1);
   int nu = 0, nv = 0;
   if (sscanf(name, "model:%dx%d", &nu, &nv) == 2 && nu >= 3 && nv >= 3)
     return model(t, asset_dir, cam, world, lights, nu, nv);

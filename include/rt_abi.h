@@ -116,6 +116,53 @@ int rt_rotate_y(rt_tree* t, int obj, double degrees);           /* RotateY trans
 int rt_constant_medium(rt_tree* t, int boundary, double density, int tex); /* medium.go:20 */
 
 /* ------------------------------------------------------------------------ */
+/* OBJ/MTL loader — LoadObjWithOptions internal/objLoader/objLoader.go:72-538, */
+/* LoadMTL + ConvertToRaytracerMaterial mtlLoader.go:53-326.  Builds the same  */
+/* triangles (bit-identical fp64 vertices/normals/uvs), the same materials and */
+/* the same two Hittables as the Go loader: *model = BuildBVH(all triangles),  */
+/* *lights = list of the emissive (and, with find_windows, dielectric) ones.   */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  const char* name;   /* map_Kd / map_Ka string exactly as written in the MTL */
+  const uint8_t* rgb; /* w*h*3, decoded by the caller (image.Decode imageLoader.go:34) */
+  int32_t w, h;
+} rt_obj_image;
+
+typedef struct {                /* LoadObjOptions objLoader.go:18-29 */
+  double scale_factor;          /* ScaleFactor */
+  int32_t flip_yz;              /* FlipYZ */
+  int32_t debug;                /* Debug: print the loader's diagnostics to stdout */
+  int32_t ignore_normals;       /* IgnoreNormals */
+  int32_t center;               /* Center (Position is applied only when set, :243-248) */
+  int32_t flip_faces;           /* FlipFaces */
+  int32_t default_material;     /* DefaultMaterial; -1 = nil -> Lambertian(.8,.8,.8) :88-90 */
+  double position[3];           /* Position */
+  int32_t ignore_mtl;           /* IgnoreMtl */
+  int32_t find_windows;         /* FindWindows */
+  /* image textures named by map_Kd / map_Ka: looked up here by exact name
+   * first; otherwise the file is opened as written (binary PPM only). */
+  int32_t n_images;
+  int32_t _pad;
+  const rt_obj_image* images;
+} rt_obj_options;
+
+typedef struct {
+  int64_t n_vertices, n_normals, n_texcoords, n_triangles, n_lights;
+  int32_t n_materials;      /* materials in the MTL library */
+  int32_t default_material; /* material id used for faces without a known usemtl */
+  double bounds_min[3], bounds_max[3], center[3]; /* after scale/flip, before centring */
+} rt_obj_info;
+
+int rt_obj_default_options(rt_obj_options* o); /* DefaultLoadOptions objLoader.go:32-45 */
+int rt_load_obj(rt_tree* t, const char* filename, const rt_obj_options* opts, int* model,
+                int* lights, rt_obj_info* info);
+/* Same from memory (e.g. a Go embed.FS); mtl_text, when non-NULL, replaces the file
+ * named by mtllib; filename (may be NULL) only resolves the mtllib directory. */
+int rt_load_obj_memory(rt_tree* t, const char* obj_text, size_t obj_len, const char* mtl_text,
+                       size_t mtl_len, const char* filename, const rt_obj_options* opts,
+                       int* model, int* lights, rt_obj_info* info);
+
+/* ------------------------------------------------------------------------ */
 /* Read-only view of a tree (consumed by the CPU oracle and the cgo shim).  */
 /* ------------------------------------------------------------------------ */
 typedef struct {

@@ -207,14 +207,35 @@ def checker(rt):
     return t, _cam(rt, (13, 2, 3), (0, 0, 0), vfov=20, bg=(0.7, 0.8, 1.0)), world, t.list(sun)
 
 
+def obj_mixed(rt, asset_dir):
+    """tests/golden/obj/mixed.obj through the OBJ/MTL loader (objLoader.go:72-538):
+    every ConvertToRaytracerMaterial branch, smooth normals, uvs, emissive and
+    image-textured triangles, rotated like modelExample (main.go:384)."""
+    import os
+    fix = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "obj")
+    obj = open(os.path.join(fix, "mixed.obj"), "rb").read()
+    tex = os.path.join(asset_dir, "earthmap.ppm")
+    mtl = open(os.path.join(fix, "mixed.mtl"), "rb").read().replace(b"@TEX@", tex.encode())
+    t = rt.Tree(1)
+    world, room_lights = _room(t)
+    o = rt.LoadObjOptions(Debug=False, ScaleFactor=1.5, Position=(0.0, 2.5, 0.0))
+    model, lights = t.LoadObjWithOptions(os.path.join(fix, "mixed.obj"), o, mtl_text=mtl,
+                                         obj_text=obj)
+    t.add(world, t.rotate_y(model, 150))
+    light = t.quad((-2, 9.9, -2), (4, 0, 0), (0, 0, 4), t.light((10, 10, 10)))
+    t.add(world, light)
+    t.add(lights, light)  # as modelExample adds its sun to the loader's light list
+    return t, _cam(rt, (0, 3, -9), (0, 2.5, 0)), world, lights
+
+
 FEATURES = ["fog", "water", "earth", "cluster", "metal_fuzz", "glass", "boxes", "marble", "motion",
             "sphere_light", "tri_mesh", "nested_lights", "smoke_box", "dup_medium", "no_lights",
-            "checker"]
+            "checker", "obj_mixed"]
 
 
 def build(rt, name, asset_dir):
     fn = globals()[name]
-    if name == "earth":
+    if name in ("earth", "obj_mixed"):
         return fn(rt, asset_dir)
     return fn(rt)
 

@@ -41,7 +41,9 @@ def test_struct_layouts_match_c(rt, tmp_path):
     from go_raytracer_amd import _lib
     structs = {"rt_camera": _lib.RtCamera, "rt_camera_derived": _lib.RtCameraDerived,
                "rt_scene_info": _lib.RtSceneInfo, "rt_render_opts": _lib.RtRenderOpts,
-               "rt_stats": _lib.RtStats, "rt_tree_view": _lib.RtTreeView}
+               "rt_stats": _lib.RtStats, "rt_tree_view": _lib.RtTreeView,
+               "rt_obj_image": _lib.RtObjImage, "rt_obj_options": _lib.RtObjOptions,
+               "rt_obj_info": _lib.RtObjInfo}
     prog = ['#include <stdio.h>', '#include "rt_abi.h"', "int main(void){"]
     for n in structs:
         prog.append(f'printf("{n} %zu\\n", sizeof({n}));')
