@@ -18,7 +18,8 @@ from ._lib import (RT_NOISE_MARBLE, RT_NOISE_PERLIN, RT_NOISE_TURBULENT, RtCamer
                    check, lib)
 
 __all__ = ["Tree", "Camera", "Scene", "quantize", "format_ppm", "device_count", "RtError",
-           "demo_scene", "DEMO_SCENES", "LoadObjOptions", "DefaultLoadOptions"]
+           "demo_scene", "DEMO_SCENES", "LoadObjOptions", "DefaultLoadOptions", "quantize_device",
+           "format_ppm_device"]
 
 DEMO_SCENES = ("book1", "book2", "book3", "simple_light", "quads", "cornell", "cornell_smoke",
                "model")
@@ -487,6 +488,37 @@ def format_ppm(rgb):
     buf = C.create_string_buffer(int(n))
     check(int(lib().rt_format_ppm(a.ctypes.data, w, h, buf, n)))
     return buf.raw[:n]
+
+
+def _stream_of(t):
+    import torch
+    return C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def quantize_device(rgb):
+    """PrintColor on a device float32 [..., 3] torch tensor -> device uint8 tensor
+    (HIP kernel, rt_quantize_device)."""
+    import torch
+    a = rgb.contiguous().to(torch.float32)
+    out = torch.empty(a.shape, dtype=torch.uint8, device=a.device)
+    check(lib().rt_quantize_device(a.data_ptr(), a.numel() // 3, out.data_ptr(),
+                                   a.device.index or 0, _stream_of(a)))
+    return out
+
+
+def format_ppm_device(rgb, to_host=True):
+    """The P3 text of camera.go:160 built on the GPU from a device float32
+    [H, W, 3] tensor (rt_format_ppm_device).  Returns bytes, or the device
+    uint8 tensor when to_host is False."""
+    import torch
+    a = rgb.contiguous().to(torch.float32)
+    h, w = a.shape[:2]
+    dev, st = a.device.index or 0, _stream_of(a)
+    n = int(lib().rt_format_ppm_device(a.data_ptr(), w, h, None, 0, dev, st))
+    check(n)
+    out = torch.empty(n, dtype=torch.uint8, device=a.device)
+    check(int(lib().rt_format_ppm_device(a.data_ptr(), w, h, out.data_ptr(), n, dev, st)))
+    return out.cpu().numpy().tobytes() if to_host else out
 
 
 def device_count():

@@ -178,6 +178,9 @@ SIGNATURES = {
                               C.POINTER(RtStats)]),
     "rt_quantize": (_I, [C.c_void_p, C.c_int64, C.c_void_p]),
     "rt_format_ppm": (C.c_int64, [C.c_void_p, _I, _I, C.c_void_p, C.c_int64]),
+    "rt_quantize_device": (_I, [C.c_void_p, C.c_int64, C.c_void_p, _I, C.c_void_p]),
+    "rt_format_ppm_device": (C.c_int64, [C.c_void_p, _I, _I, C.c_void_p, C.c_int64, _I,
+                                         C.c_void_p]),
     "rt_demo_scene": (_I, [_P, C.c_char_p, C.c_char_p, C.POINTER(RtCamera), C.POINTER(_I),
                            C.POINTER(_I)]),
     "rt_demo_scene_name": (_I, [_I, C.POINTER(C.c_char_p)]),

@@ -364,6 +364,15 @@ int rt_quantize(const float* rgb, int64_t n_pixels, uint8_t* out);
  * (call with out = NULL to size). */
 int64_t rt_format_ppm(const float* rgb, int w, int h, char* out, int64_t cap);
 
+/* On-device output (HIP): the same PrintColor bytes / P3 text, produced by kernels
+ * from an image already in HBM (rgb_dev: device fp32 [n][3] on `device`; out_dev:
+ * device memory; stream: hipStream_t or NULL).  The calls return after the work
+ * completes.  rt_format_ppm_device returns the byte count (out_dev = NULL to size). */
+int rt_quantize_device(const float* rgb_dev, int64_t n_pixels, uint8_t* out_dev, int device,
+                       void* stream);
+int64_t rt_format_ppm_device(const float* rgb_dev, int w, int h, char* out_dev, int64_t cap,
+                             int device, void* stream);
+
 /* Demo scenes mirroring main.go (by name or the main.go -S number).
  * names: book1, book2, book3, simple_light, quads, cornell, cornell_smoke, model
  * The camera receives the scene's settings; override fields afterwards. */

@@ -159,12 +159,12 @@ def test_hand_derived_expectations(rt, mixed):
     t = rt.Tree()
     model, lights = t.LoadObjWithOptions(str(d / "mixed.obj"), rt.LoadObjOptions(Debug=False))
     tris, lidx = tree_triangles(t, model, lights)
-    # bounds of the 6 vertices: x [-1, 2], y [0, 3], z [-1, 0.5] -> centre (0.5, 1.5, -0.25)
+    # bounds of the 39 vertices: x [-3, 5], y [-3, 5], z [-3.5, 3.5] -> centre (1, 1, 0)
     info = t.last_obj_info
-    assert list(info.center) == [0.5, 1.5, -0.25]
+    assert list(info.center) == [1.0, 1.0, 0.0]
     # first face "f 1/1/1 2/2/1 3/3/2 4/4/2": fan (1,2,3), (1,3,4), centred
-    assert tris[0][0] == [-0.5, -1.5, 0.25, 1.5, -1.5, 0.25, 1.5, 0.5, 0.25]
-    assert tris[1][0] == [-0.5, -1.5, 0.25, 1.5, 0.5, 0.25, -0.5, 0.5, 0.25]
+    assert tris[0][0] == [-1.0, -1.0, 0.0, 1.0, -1.0, 0.0, 1.0, 1.0, 0.0]
+    assert tris[1][0] == [-1.0, -1.0, 0.0, 1.0, 1.0, 0.0, -1.0, 1.0, 0.0]
     assert tris[0][2] == [0, 0, 1, 0, 1, 1] and tris[1][2] == [0, 0, 1, 1, 0, 1]
     s = 1 / math.sqrt(2)
     assert tris[0][1] == [0, 0, 1, 0, 0, 1, 0, s, s]  # vn normalised by x * (1/len)
@@ -172,9 +172,9 @@ def test_hand_derived_expectations(rt, mixed):
     # pentagon: 3 fan triangles, normals only, gold metal: fuzz (1 - 250/1000)^2
     assert [x[2] for x in tris[2:5]] == [None] * 3 and all(x[1] for x in tris[2:5])
     assert tris[2][3] == ("metal", (1.0, 0.843, 0.0), 0.5625)
-    # "f -1 -2 -3" -> vertices 6, 5, 4 (relative to the total count); "f 0 2 99" -> 1, 2, 6
-    assert tris[5][0][:3] == [-1.5, 1.0, 0.75] and tris[5][3] == ("dielectric", 1.45)
-    assert tris[6][0][:3] == [-0.5, -1.5, 0.25] and tris[6][0][6:] == [-1.5, 1.0, 0.75]
+    # "f -1 -2 -3" -> vertices 39, 38, 37 (relative to the total count); "f 0 2 99" -> 1, 2, 39
+    assert tris[5][0][:3] == [-0.5, 1.0, 3.0] and tris[5][3] == ("dielectric", 1.45)
+    assert tris[6][0][:3] == [-1.0, -1.0, 0.0] and tris[6][0][6:] == [-0.5, 1.0, 3.0]
     # unknown material -> the default Lambertian(0.8); uv but no normals
     assert tris[7][3] == ("lambertian", (0.8, 0.8, 0.8)) and tris[7][1] is None
     # "f 4//3 ..." where vn 3 is defined just before: normal (1,0,0); lamp is a light
