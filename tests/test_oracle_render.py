@@ -53,3 +53,16 @@ def test_maxcontribution_clamp(rt, oracle):
     # first-vertex light hits are unclamped emission (15,15,15); everything else <= 1.5
     s = img.sum(axis=2)
     assert (s[(s > 0) & (s < 40)] <= 1.5 + 1e-5).mean() > 0.5
+
+
+def test_obj_fixture_is_well_conditioned(rt, oracle):
+    """The OBJ feature scene must not decide hits by rounding (coplanar overlapping
+    faces would make fp32-vs-fp64 parity meaningless): the fp32 twin agrees."""
+    import os
+    t, cam, w, l = scenes.build(rt, "obj_mixed",
+                                os.path.join(os.path.dirname(scenes.__file__), "..", "assets"))
+    a, sa = oracle.render(t, w, l, cam, seed=11, threads=8, precision=64)
+    b, sb = oracle.render(t, w, l, cam, seed=11, threads=8, precision=32)
+    assert sa["segments"] == sb["segments"]
+    close = np.abs(a - b) <= 1e-3 * np.maximum(1.0, np.abs(a))
+    assert close.mean() >= 0.999
