@@ -387,6 +387,13 @@ class Scene:
     def __exit__(self, *a):
         self.close()
 
+    def progress(self):
+        """(samples done, samples total) of the render in flight (rt_progress);
+        callable from another thread while render() blocks."""
+        d, t = C.c_uint64(0), C.c_uint64(0)
+        check(lib().rt_progress(self._p, C.byref(d), C.byref(t)))
+        return d.value, t.value
+
     def info(self):
         i = RtSceneInfo()
         check(lib().rt_scene_info_get(self._p, C.byref(i)))
@@ -422,8 +429,11 @@ class Scene:
         return o
 
     def render(self, camera, seed=1, device=0, rank=0, nranks=1, path_slots=0, chunk=0,
-               profile=False, trace=None, mode="auto"):
+               profile=False, trace=None, mode="auto", progress_slices=0):
         """Render this rank's rows -> (float32 [rows, W, 3], stats dict).
+
+        progress_slices=S runs the fused render as S launches so that progress()
+        (from another thread) advances per slice; the image is the same.
 
         trace=(pixel, sample) additionally returns stats["trace"]: float32 [V, 12]
         {o.xyz, time, d.xyz, vertex, t, u, v, ref bits} per world.Hit of that sample.
@@ -434,6 +444,7 @@ class Scene:
         st = RtStats()
         c = camera.to_c()
         o = self._opts(seed, device, rank, nranks, path_slots, chunk, profile, None, mode)
+        o.progress_slices = progress_slices
         tbuf = None
         if trace is not None:
             tbuf = np.zeros((d.max_depth + 1, 12), np.float32)

@@ -2,7 +2,9 @@
 #pragma once
 #include <stdint.h>
 
+#include <atomic>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -66,11 +68,24 @@ struct HostScene {
 struct DeviceScene;  // defined in the HIP translation unit
 struct RenderState;
 
+// Progress of the render in flight (rt_progress): written by the rendering
+// thread, read by any polling thread under `mu`.
+struct Progress {
+  std::mutex mu;
+  int busy = 0;                 // 1 while a render is in flight
+  int device = -1;
+  uint64_t total = 0;           // samples of the current / last render
+  uint64_t done = 0;            // samples of the last render once it returned
+  std::vector<void*> events;    // hipEvent_t recorded after each slice
+  std::vector<uint64_t> cum;    // samples complete when event i has fired
+};
+
 struct Scene {
   HostScene h;
   int device = -1;
   DeviceScene* dev = nullptr;     // uploaded lazily by rt_render
   RenderState* state = nullptr;   // wavefront buffers, reused across renders
+  Progress prog;
 };
 
 // host_flatten.cpp

@@ -107,9 +107,10 @@ RT_D Ids chunk_ids(const Params& P, uint32_t chunk) {
   return r;
 }
 
-// getRay camera.go:256-270 + sampleSquareStratified :277-282 + defocusDiskSample :285-290
-RT_D void camera_ray(const Params& P, const Ids& id, uint32_t sample, f3& o, f3& d, float& time) {
-  rt_u32x4 r = rt_rng_draw(P.seed, id.gpix, sample, RT_STREAM_CAMERA);
+// getRay camera.go:256-270 + sampleSquareStratified :277-282 + defocusDiskSample :285-290;
+// r = rt_rng_draw(seed, gpix, sample, RT_STREAM_CAMERA), drawn by the caller
+RT_D void camera_ray_r(const Params& P, const Ids& id, uint32_t sample, const rt_u32x4& r, f3& o,
+                       f3& d, float& time) {
   uint32_t si = fdiv(sample, P.fd_s), sj = sample - si * (uint32_t)P.s;
   float px = (((float)sj + rt_unit_f(r.v[0])) * P.recip_s) - 0.5f;
   float py = (((float)si + rt_unit_f(r.v[1])) * P.recip_s) - 0.5f;
@@ -127,6 +128,9 @@ RT_D void camera_ray(const Params& P, const Ids& id, uint32_t sample, f3& o, f3&
     d = d - off;
   }
   time = rt_unit_f(r.v[2]);
+}
+RT_D void camera_ray(const Params& P, const Ids& id, uint32_t sample, f3& o, f3& d, float& time) {
+  camera_ray_r(P, id, sample, rt_rng_draw(P.seed, id.gpix, sample, RT_STREAM_CAMERA), o, d, time);
 }
 
 // ------------------------------------------------------------- traversal ---
@@ -820,6 +824,22 @@ RT_D void load_path(const Params& P, uint32_t slot, Path& s) {
   s.flags = ps.y >> 28;
 }
 
+// the next sample of the same chunk, its camera draw already made: the path
+// state (pixel ids cached in s) is reset for sample j
+template <bool SOA>
+RT_D void next_sample(const Params& P, uint32_t slot, Path& s, uint32_t j, const rt_u32x4& r) {
+  Ids id;
+  id.gpix = s.gpix;
+  id.row = fdiv(s.gpix, P.fd_width);
+  id.col = s.gpix - id.row * (uint32_t)P.width;
+  camera_ray_r(P, id, s.s0 + j, r, s.o, s.d, s.time);
+  s.j = j;
+  s.k = 0;
+  s.nst = 0;
+  s.flags = 0;
+  store_ray<SOA>(P, slot, s);
+}
+
 // camera ray for sample j of `chunk` (path state reset)
 template <bool SOA>
 RT_D void start_sample(const Params& P, uint32_t slot, Path& s, uint32_t chunk, uint32_t j) {
@@ -845,18 +865,19 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
   const uint32_t ref = h.ref;
   f3 lterm = mk3(0, 0, 0);
   bool term = false;
-  if (ref == PRIM_NONE) {
-    lterm = mk3(P.bg[0], P.bg[1], P.bg[2]);  // camera.go:300-302
-    term = true;
-  } else {
+  rt_u32x4 rcam;  // camera draw of the next sample, when this vertex made it
+  bool have_rcam = false;
+  f3 p = mk3(0, 0, 0), n = mk3(0, 0, 0);
+  float u = h.u, v = h.v;
+  bool ff = true;
+  DevMaterial M;
+  bool scat = false;
+  if (ref != PRIM_NONE) {
     const float t = h.t;
-    const f3 p = o + d * t;  // r.At(t)
+    p = o + d * t;  // r.At(t)
     const uint32_t type = ref >> 30, idx = ref & 0x3FFFFFFFu;
     f3 nout;
-    float u = h.u, v = h.v;
     int mat;
-    bool ff = true;
-    f3 n;
     if (HAS(FT_SPHERE) && type == PRIM_SPHERE) {
       const F4 cr = sc.sph_cr[idx], mv = sc.sph_mv[idx];
       f3 cc = xyz(cr) + xyz(mv) * time;
@@ -898,12 +919,32 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
       ff = true;
       u = v = 0.0f;
     }
-    const DevMaterial M = sc.mats[mat];
-    if (M.kind == RT_MAT_DIFFUSE_LIGHT) {  // Emitted materials.go:150-155; Scatter false
+    M = sc.mats[mat];
+    scat = M.kind != RT_MAT_DIFFUSE_LIGHT;
+  }
+  // ONE Philox call per vertex for the whole wave: a scattering vertex draws its
+  // own numbers; a path ending here (miss or light) draws the camera numbers of
+  // the chunk's next sample (otherwise two divergent calls per iteration):
+  // C2 +3 %, C3 +2 %.  The all-features kernel (3 waves/SIMD, register-bound)
+  // keeps the two draws in their branches (merged there: C4 -3 %).
+  constexpr bool kMergeDraws = FT != FT_ALL;
+  rt_u32x4 r;
+  if (kMergeDraws)
+    r = rt_rng_draw(P.seed, s.gpix, s.s0 + s.j + (scat ? 0u : 1u),
+                    scat ? RT_STREAM(s.k, 0) : RT_STREAM_CAMERA);
+  if (!scat) {
+    if (ref == PRIM_NONE)
+      lterm = mk3(P.bg[0], P.bg[1], P.bg[2]);  // camera.go:300-302
+    else  // Emitted materials.go:150-155; Scatter false
       lterm = ff ? tex_value<FT>(sc, M.tex, u, v, p) : mk3(0, 0, 0);
-      term = true;
-    } else {
-      const rt_u32x4 r = rt_rng_draw(P.seed, s.gpix, s.s0 + s.j, RT_STREAM(s.k, 0));
+    term = true;
+    if (kMergeDraws) {
+      rcam = r;
+      have_rcam = true;
+    }
+  } else {
+    if (!kMergeDraws) r = rt_rng_draw(P.seed, s.gpix, s.s0 + s.j, RT_STREAM(s.k, 0));
+    {
       f3 ndir;
       bool clamp_vertex = false;
       f3 weight;
@@ -998,7 +1039,9 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
   const uint32_t count = min(P.K, P.ss - s.s0);  // chunk_ids().count
   if (s.j + 1 < count) {
     set_acc<SOA>(P, slot, s, acc);
-    start_sample<SOA>(P, slot, s, s.chunk, s.j + 1);
+    if (!have_rcam)  // a miss, or the depth limit: the camera draw is made here
+      rcam = rt_rng_draw(P.seed, s.gpix, s.s0 + s.j + 1, RT_STREAM_CAMERA);
+    next_sample<SOA>(P, slot, s, s.j + 1, rcam);
     return OUT_ALIVE;
   }
   flush_chunk(P, s.chunk, acc);

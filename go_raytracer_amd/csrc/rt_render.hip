@@ -312,6 +312,7 @@ struct RenderState {
   float* out = nullptr;
   uint32_t out_cap = 0;
   std::vector<hipEvent_t> events;
+  std::vector<hipEvent_t> prog_events;  // one per progress slice (rt_progress)
   int resident_blocks = 0;
   void free_all() {
     for (void* p : allocs) (void)hipFree(p);
@@ -320,6 +321,7 @@ struct RenderState {
   ~RenderState() {
     free_all();
     for (auto e : events) (void)hipEventDestroy(e);
+    for (auto e : prog_events) (void)hipEventDestroy(e);
     if (own_stream) (void)hipStreamDestroy(own_stream);
   }
 };
@@ -817,6 +819,41 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   }
   int iterations = 0;
   int n_ext = 0, n_sh = 0;
+  // rt_progress: the fused render as `slices` launches over consecutive chunk
+  // ranges, an event after each (the image does not depend on the split)
+  const int slices = (mode == RT_MODE_FUSED && n_chunks > 0)
+                         ? std::max(1, std::min(o.progress_slices, 1024))
+                         : 1;
+  while ((int)st->prog_events.size() < slices) {
+    hipEvent_t e;
+    HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    st->prog_events.push_back(e);
+  }
+  {
+    std::lock_guard<std::mutex> lk(s->prog.mu);
+    s->prog.total = (uint64_t)npix * ss;
+    s->prog.done = 0;
+    s->prog.device = o.device;
+    s->prog.events.clear();
+    s->prog.cum.clear();
+    if (slices > 1)
+      for (int sl = 0; sl < slices; ++sl) {
+        s->prog.events.push_back((void*)st->prog_events[sl]);
+        s->prog.cum.push_back((uint64_t)((double)s->prog.total *
+                                         (double)((uint64_t)n_chunks * (sl + 1) / slices) /
+                                         (double)n_chunks));
+      }
+    s->prog.busy = 1;
+  }
+  struct ProgressDone {  // every return path below ends the in-flight state
+    Progress& p;
+    bool ok = false;
+    ~ProgressDone() {
+      std::lock_guard<std::mutex> lk(p.mu);
+      if (ok) p.done = p.total;
+      p.busy = 0;
+    }
+  } prog_done{s->prog};
   if (n_chunks > 0 && mode == RT_MODE_FUSED) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (prof) {
@@ -824,8 +861,18 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
       HIP_OK(hipEventRecord(e0, stream));
     }
     void* args[] = {&p};
-    HIP_OK(hipLaunchKernel(fused_kernel, dim3(fused_blocks), dim3(256), args, fused_lds, stream));
-    HIP_OK(hipGetLastError());
+    for (int sl = 0; sl < slices; ++sl) {
+      if (slices > 1) {  // chunks [n*sl/S, n*(sl+1)/S): the counter starts at the range
+        p.n_chunks = (uint32_t)((uint64_t)n_chunks * (sl + 1) / slices);
+        if (sl > 0)
+          HIP_OK(hipMemsetD32Async((hipDeviceptr_t)&st->ctr->chunk_head,
+                                   (int)((uint64_t)n_chunks * sl / slices), 1, stream));
+      }
+      HIP_OK(hipLaunchKernel(fused_kernel, dim3(fused_blocks), dim3(256), args, fused_lds, stream));
+      HIP_OK(hipGetLastError());
+      if (slices > 1) HIP_OK(hipEventRecord(st->prog_events[sl], stream));
+    }
+    p.n_chunks = n_chunks;
     if (prof) {
       HIP_OK(hipEventRecord(e1, stream));
       ev_fused.push_back({ev_used - 2, ev_used - 1});
@@ -881,6 +928,7 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     HIP_OK(hipMemcpyAsync(out_host, dst, 3 * (size_t)npix * sizeof(float), hipMemcpyDeviceToHost,
                           stream));
   HIP_OK(hipStreamSynchronize(stream));
+  prog_done.ok = true;
   auto t_end = std::chrono::steady_clock::now();
   if (dtrace) {
     HIP_OK(hipMemcpy(o.trace_out, dtrace, (size_t)o.trace_cap * 3 * sizeof(F4), hipMemcpyDeviceToHost));
@@ -939,6 +987,21 @@ int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_render_opts* op
                      float* out_rgb_device, rt_stats* stats) {
   if (!out_rgb_device) return rt::set_error(RT_ERR_INVALID, "rt_render_device: null output");
   return rt::render_impl(s, cam, opts, nullptr, out_rgb_device, stats);
+}
+
+int rt_progress(const rt_scene* sc, uint64_t* done, uint64_t* total) {
+  if (!sc || !done || !total) return rt::set_error(RT_ERR_INVALID, "rt_progress: null");
+  rt::Progress& p = const_cast<rt_scene*>(sc)->s.prog;
+  std::lock_guard<std::mutex> lk(p.mu);
+  *total = p.total;
+  *done = p.busy ? 0 : p.done;
+  if (!p.busy || p.events.empty()) return RT_OK;
+  if (hipSetDevice(p.device) != hipSuccess) return rt::set_error(RT_ERR_DEVICE, "rt_progress");
+  for (size_t i = 0; i < p.events.size(); ++i) {  // slices complete in stream order
+    if (hipEventQuery((hipEvent_t)p.events[i]) != hipSuccess) break;
+    *done = p.cum[i];
+  }
+  return RT_OK;
 }
 
 int rt_device_count(void) {

@@ -322,6 +322,11 @@ typedef struct {
   int32_t trace_sample;
   int32_t trace_cap;
   float* trace_out;
+  /* rt_progress granularity: the fused render runs as this many launches over
+   * consecutive chunk ranges (same image, bit for bit) and rt_progress advances
+   * as each completes.  0/1 = one launch, progress only reports start and end. */
+  int32_t progress_slices;
+  int32_t _pad3;
 } rt_render_opts;
 
 typedef struct {
@@ -357,6 +362,13 @@ int rt_render(rt_scene* s, const rt_camera* cam, const rt_render_opts* opts, flo
  * work is enqueued on opts->stream and the call returns after it completes. */
 int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_render_opts* opts,
                      float* out_rgb_device, rt_stats* stats);
+
+/* Progress of the render in flight on scene s (the reference's progress bar,
+ * camera.go:106-108 + internal/progress): may be polled from any thread while
+ * rt_render blocks in another.  *total = samples of the current (or last)
+ * render; *done = samples of the completed slices (opts.progress_slices), and
+ * *total once the render returned. */
+int rt_progress(const rt_scene* s, uint64_t* done, uint64_t* total);
 
 /* Output: PrintColor vec/color.go:23-46 (NaN->0, sqrt gamma, clamp .99999, x256). */
 int rt_quantize(const float* rgb, int64_t n_pixels, uint8_t* out);

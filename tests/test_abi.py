@@ -70,3 +70,9 @@ def test_errors_are_codes_not_aborts(rt):
 
 def test_device_count_never_aborts(rt):
     assert rt.device_count() >= 0
+
+
+def test_progress_without_render(rt):
+    t, cam, w, l = rt.demo_scene("cornell")
+    with rt.Scene(t, w, l) as sc:
+        assert sc.progress() == (0, 0)

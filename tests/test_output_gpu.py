@@ -80,3 +80,34 @@ def test_render_to_ppm_on_device(rt, gpu):
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), img)
     assert rt.format_ppm_device(out) == rt.format_ppm(img)
+
+
+def test_progress_while_rendering(rt, gpu):
+    """rt_progress polled from another thread sees the render advance slice by slice
+    (the reference's progress bar, camera.go:106-108); slicing leaves the image
+    bit-identical and progress reports completion afterwards."""
+    import threading
+    import time
+    t, cam, w, l = rt.demo_scene("cornell")
+    cam.Width, cam.SamplesPerPixel = 800, 1024
+    seen = []
+    with rt.Scene(t, w, l) as sc:
+        ref, _ = sc.render(cam, seed=1)
+        assert sc.progress() == (655360000, 655360000)
+        stop = threading.Event()
+
+        def poll():
+            while not stop.is_set():
+                seen.append(sc.progress())
+                time.sleep(0.0005)
+        th = threading.Thread(target=poll)
+        th.start()
+        img, st = sc.render(cam, seed=1, progress_slices=16)
+        stop.set()
+        th.join()
+        done, total = sc.progress()
+    assert np.array_equal(img, ref)
+    assert total == st["samples"] == done
+    mid = sorted({d for d, tt in seen if 0 < d < total})
+    assert len(mid) >= 4, seen[:40]
+    assert all(0 <= d <= tt for d, tt in seen)
