@@ -56,6 +56,7 @@ struct Params {
   uint32_t ss;         // s*s
   int step_budget;     // fused: traversal steps per scheduling round
   uint32_t shade_min;  // fused: lanes that must be waiting before a wave shades
+  uint32_t grab_min;   // fused: chunks a wave takes per refill of its batch (>= 1)
   uint32_t recs_lds;   // leaf records cached in LDS after the nodes (stage_nodes)
   uint64_t seed;
   // wavefront state (SoA, slot-indexed)
@@ -1050,8 +1051,10 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
 
 // Wave-batched work distribution: lanes that need a chunk take consecutive ids
 // from the wave's current batch; the batch is refilled with ONE returning
-// atomic per 64+ chunks (a single counter saturates near 88 returning atomics
-// per µs on MI355X, so per-event atomics would serialise the whole chip).
+// atomic per >= grab_min chunks (a single counter saturates near 88 returning
+// atomics per µs on MI355X, so per-event atomics would serialise the whole chip;
+// 8-GPU share of C2: 41 ms with 1-chunk grabs, 8.0 ms with 64).  Splitting the
+// range over 8 partition counters measured 6-12 % slower (C2, 1 and 8 ranks).
 struct WaveBatch {
   uint32_t next, end;  // wave-uniform
 };
@@ -1066,7 +1069,7 @@ RT_D uint32_t grab_chunk(const Params& P, WaveBatch& b, bool need) {
     mine = b.next + r;
     b.next += n;
   } else {
-    const uint32_t grab = max(64u, n - avail);
+    const uint32_t grab = max(P.grab_min, n - avail);
     uint32_t g = 0;
     if (lane_id() == (uint32_t)(__ffsll((long long)m) - 1)) g = atomicAdd(&P.ctr->chunk_head, grab);
     g = __shfl(g, __ffsll((long long)m) - 1);

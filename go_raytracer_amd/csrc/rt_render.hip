@@ -168,6 +168,9 @@ __global__ __launch_bounds__(256) void k_init(Params P) {
 // FT = compiled-in scene features (rt_device.h), chosen per scene by pick_fused.
 // Waves per SIMD by feature set: the lean sets fit more waves in the register
 // file (VGPRs <= 512 / waves) and in LDS (24 KB static + the scene cache).
+#ifndef FT_TEX_WAVES
+#define FT_TEX_WAVES 4
+#endif
 #ifndef BRUTE_WAVES
 #define BRUTE_WAVES 6
 #endif
@@ -177,7 +180,9 @@ constexpr int fused_waves(uint32_t ft, int tree = 4) {
   return (tree == 0 && ft == 0u) ? kBruteWaves  // 7 measured within noise of 6, 8 -3 %
          : ft == 0u ? 6
          : ft == FT_MEDIA ? 4
-         : ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? 4 : 3;
+         : ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? 4
+         : ft == (FT_SPHERE | FT_METAL | FT_DIEL | FT_MEDIA | FT_IMAGE | FT_NOISE) ? FT_TEX_WAVES
+                                                                                  : 3;
 }
 // LDS clamp-weight entries (12 B each): 6 (C2 +1 %, C3 +2.5 % over 3-4), 4 for the
 // mesh set, whose specular paths rarely push weights (C5 -1.5 % with 6)
@@ -556,6 +561,7 @@ static constexpr uint32_t kFtSets[] = {
     0u,                                                     // Cornell box: quads, Lambertian, light
     FT_MEDIA,                                               // + constant media (Cornell smoke)
     FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER,   // meshes and spheres, plain materials
+    FT_SPHERE | FT_METAL | FT_DIEL | FT_MEDIA | FT_IMAGE | FT_NOISE,  // spheres, media, textures
     FT_ALL};
 static_assert(FT_SPHERE == RT_FT_SPHERE && FT_TRI == RT_FT_TRI && FT_METAL == RT_FT_METAL &&
                   FT_DIEL == RT_FT_DIEL && FT_MEDIA == RT_FT_MEDIA && FT_CHECKER == RT_FT_CHECKER &&
@@ -568,6 +574,7 @@ static const void* fused_for(uint32_t set) {
     case kFtSets[0]: return (const void*)k_fused<LDS, kFtSets[0], 4>;
     case kFtSets[1]: return (const void*)k_fused<LDS, kFtSets[1], 4>;
     case kFtSets[2]: return (const void*)k_fused<LDS, kFtSets[2], 4>;
+    case kFtSets[3]: return (const void*)k_fused<LDS, kFtSets[3], 4>;
     default: return (const void*)k_fused<LDS, FT_ALL, 4>;
   }
 }
@@ -770,6 +777,10 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   // kernel, whose shading is long, also gains from shading 32+ lanes at once.
   p.step_budget = env_int("RT_STEP_BUDGET", f_lds ? (1 << 30) : 8);
   p.shade_min = (uint32_t)env_int("RT_SHADE_MIN", !f_lds && ft_set == FT_ALL ? 32 : 1);
+  // chunks per refill of a wave's batch (one returning atomic on the chunk
+  // counter each): C2 grab sweep (profiles/r1_grab_sweep.jsonl) 64 -> 128:
+  // -4 % at 1-2 ranks' shares; 256 for small chunks: -11 % on the 8-GPU share
+  p.grab_min = (uint32_t)std::max(1, env_int("RT_GRAB_MIN", K <= 8u ? 256 : 128));
   p.recs_lds = f_recs ? 1u : 0u;
   p.seed = o.seed;
   p.ray_o = st->ray_o;
