@@ -57,6 +57,7 @@ struct Params {
   int step_budget;     // fused: traversal steps per scheduling round
   uint32_t shade_min;  // fused: lanes that must be waiting before a wave shades
   uint32_t grab_min;   // fused: chunks a wave takes per refill of its batch (>= 1)
+  unsigned long long* wave_times;  // debug (RT_WAVE_TIMES): per wave {start, end, segments}
   uint32_t recs_lds;   // leaf records cached in LDS after the nodes (stage_nodes)
   uint64_t seed;
   // wavefront state (SoA, slot-indexed)
@@ -1069,6 +1070,8 @@ RT_D uint32_t grab_chunk(const Params& P, WaveBatch& b, bool need) {
     mine = b.next + r;
     b.next += n;
   } else {
+    // (shrinking the batch as the pool drains measured 10-30 % slower: once a
+    // wave refills every iteration the counter saturates; profiles/r1_wave_timeline.jsonl)
     const uint32_t grab = max(P.grab_min, n - avail);
     uint32_t g = 0;
     if (lane_id() == (uint32_t)(__ffsll((long long)m) - 1)) g = atomicAdd(&P.ctr->chunk_head, grab);

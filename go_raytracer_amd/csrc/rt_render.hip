@@ -214,6 +214,7 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
   tr.cur = TRAV_DONE;
   bool has = false;
   WaveBatch b = {0u, 0u};
+  const unsigned long long t_start = P.wave_times ? wall_clock64() : 0ull;
   // Scheduling round: lanes without work take a chunk; traversing lanes run up
   // to step_budget traversal steps; lanes whose traversal is done are shaded
   // together once at least shade_min of them wait (or nothing else traverses),
@@ -255,6 +256,12 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
   if (lane_id() == 0) {
     atomicAdd(&P.ctr->segments, (unsigned long long)segs);
     atomicAdd(&P.ctr->pushes, (unsigned long long)pushes);
+    if (P.wave_times) {
+      const size_t w = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+      P.wave_times[3 * w] = t_start;
+      P.wave_times[3 * w + 1] = wall_clock64();
+      P.wave_times[3 * w + 2] = segs;
+    }
   }
 }
 
@@ -781,6 +788,7 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   // counter each): C2 grab sweep (profiles/r1_grab_sweep.jsonl) 64 -> 128:
   // -4 % at 1-2 ranks' shares; 256 for small chunks: -11 % on the 8-GPU share
   p.grab_min = (uint32_t)std::max(1, env_int("RT_GRAB_MIN", K <= 8u ? 256 : 128));
+  p.wave_times = nullptr;
   p.recs_lds = f_recs ? 1u : 0u;
   p.seed = o.seed;
   p.ray_o = st->ray_o;
@@ -871,6 +879,14 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
       if ((rc = next_event(&e0)) || (rc = next_event(&e1))) return rc;
       HIP_OK(hipEventRecord(e0, stream));
     }
+    // debug: per-wave start/end clocks (100 MHz) + chunks -> binary file RT_WAVE_TIMES
+    const char* wt_path = getenv("RT_WAVE_TIMES");
+    unsigned long long* wt = nullptr;
+    const size_t n_waves = (size_t)fused_blocks * 4;
+    if (wt_path && *wt_path) {
+      HIP_OK(hipMalloc(&wt, 3 * n_waves * sizeof(unsigned long long)));
+      p.wave_times = wt;
+    }
     void* args[] = {&p};
     for (int sl = 0; sl < slices; ++sl) {
       if (slices > 1) {  // chunks [n*sl/S, n*(sl+1)/S): the counter starts at the range
@@ -884,6 +900,17 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
       if (slices > 1) HIP_OK(hipEventRecord(st->prog_events[sl], stream));
     }
     p.n_chunks = n_chunks;
+    if (wt) {
+      std::vector<unsigned long long> h(3 * n_waves);
+      HIP_OK(hipMemcpyAsync(h.data(), wt, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost, stream));
+      HIP_OK(hipStreamSynchronize(stream));
+      HIP_OK(hipFree(wt));
+      p.wave_times = nullptr;
+      if (FILE* f = fopen(wt_path, "wb")) {
+        fwrite(h.data(), sizeof(h[0]), h.size(), f);
+        fclose(f);
+      }
+    }
     if (prof) {
       HIP_OK(hipEventRecord(e1, stream));
       ev_fused.push_back({ev_used - 2, ev_used - 1});

@@ -1,0 +1,37 @@
+#!/usr/bin/env python3
+"""Wave timeline of the fused kernel (dev tool): renders C2 shares with
+RT_WAVE_TIMES set and summarises when waves finish relative to the kernel span.
+usage: python3 tools/wave_timeline.py [nranks ...]"""
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import go_raytracer_amd as rt  # noqa: E402
+
+t, cam, w, l = rt.demo_scene("cornell")
+cam.Width, cam.SamplesPerPixel = 800, 1024
+path = "/tmp/wave_times.bin"
+with rt.Scene(t, w, l) as sc:
+    for n in [int(x) for x in sys.argv[1:]] or [1, 8]:
+        sc.render(cam, nranks=n)
+        os.environ["RT_WAVE_TIMES"] = path
+        img, st = sc.render(cam, nranks=n, profile=True)
+        os.environ.pop("RT_WAVE_TIMES")
+        a = np.fromfile(path, dtype=np.uint64).reshape(-1, 3).astype(np.int64)
+        t0 = a[:, 0].min()
+        start = (a[:, 0] - t0) / 100.0  # 100 MHz -> µs
+        end = (a[:, 1] - t0) / 100.0
+        span = end.max()
+        q = lambda x, p: float(np.percentile(x, p))  # noqa: E731
+        print(json.dumps({
+            "nranks": n, "kernel_ms": round(st["ms_fused"], 3), "waves": len(a),
+            "span_us": round(span, 1), "start_p50_us": round(q(start, 50), 1),
+            "start_max_us": round(start.max(), 1),
+            "end_p1_us": round(q(end, 1), 1), "end_p10_us": round(q(end, 10), 1),
+            "end_p50_us": round(q(end, 50), 1), "end_p90_us": round(q(end, 90), 1),
+            "idle_frac": round(float(np.sum(span - end) / (span * len(a))), 4),
+            "segments_p50": q(a[:, 2], 50), "segments_min": int(a[:, 2].min()),
+            "segments_max": int(a[:, 2].max())}), flush=True)
