@@ -246,15 +246,15 @@ def _mtl_image_names(filename, mtl_text):
     if text is None:
         if filename is None or not os.path.exists(filename):
             return []
-        lib_name = None
+        import re
         with open(filename, "rb") as f:
-            for raw in f:
-                p = raw.decode("utf-8", "replace").split()
-                if len(p) >= 2 and p[0] == "mtllib":
-                    lib_name = " ".join(p[1:])
-                    break
-        if lib_name is None:
+            data = f.read()
+        k = data.find(b"mtllib")  # C-speed scan first: most meshes have none
+        m = None if k < 0 else re.search(rb"^[ \t]*mtllib[ \t]+([^\r\n]+)",
+                                         data[max(0, data.rfind(b"\n", 0, k) + 1):], re.M)
+        if m is None:
             return []
+        lib_name = " ".join(m.group(1).decode("utf-8", "replace").split())
         path = os.path.join(os.path.dirname(filename), lib_name)
         if not os.path.exists(path):
             return []

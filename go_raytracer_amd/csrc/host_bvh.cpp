@@ -11,7 +11,13 @@
 
 #include <algorithm>
 #include <array>
+#include <stdio.h>
+
+#include <atomic>
+#include <chrono>
 #include <deque>
+#include <thread>
+#include <vector>
 
 #include "rt_internal.h"
 
@@ -93,41 +99,98 @@ int build_bvh(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi
   }
   std::vector<int> idx(n);
   for (int i = 0; i < n; ++i) idx[i] = i;
+  const bool timing = getenv("RT_TIMING") != nullptr;
+  auto tic = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    if (!timing) return;
+    auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "[rt]   bvh %s %.3f s\n", what, std::chrono::duration<double>(now - tic).count());
+    tic = now;
+  };
 
-  std::vector<TmpNode> tn;
-  tn.reserve(2 * (size_t)n / kLeafTarget + 16);
-  tn.push_back(TmpNode());
-  tn[0].first = 0;
-  tn[0].count = n;
-  std::vector<int> work = {0};
-  while (!work.empty()) {
-    int ni = work.back();
-    work.pop_back();
-    TmpNode& nd = tn[ni];
+  // Node split: bounds, binned SAH over three axes, partition of idx[first,
+  // first+count).  Box growth is min/max and bin counts are integers, so running
+  // the loops on T threads (large nodes) gives bit-identical trees.
+  const int threads = std::max(1, std::min(env_i("RT_THREADS", env_i("OMP_NUM_THREADS", 16)),
+                                           (int)std::max(1u, std::thread::hardware_concurrency())));
+  auto par = [&](int T, int first, int count, auto&& fn) {  // fn(t, lo, hi)
+    if (T <= 1) {
+      fn(0, first, first + count);
+      return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t) {
+      const int lo = first + (int)((int64_t)count * t / T), hi = first + (int)((int64_t)count * (t + 1) / T);
+      th.emplace_back([&fn, t, lo, hi] { fn(t, lo, hi); });
+    }
+    for (auto& x : th) x.join();
+  };
+  // returns true and fills L, R when nd is split (nd.box is always set)
+  auto split_node = [&](TmpNode& nd, int T, TmpNode& L, TmpNode& R) -> bool {
+    // per-thread partials: on the stack for the one-thread case (every node below
+    // the top levels), on the heap otherwise (few, large nodes)
+    Box pbb1[1], pcb1[1];
+    std::array<Box, 3 * kBins> tbins1[1];
+    std::array<int, 3 * kBins> tcnt1[1];
+    std::vector<Box> pbbv, pcbv;
+    std::vector<std::array<Box, 3 * kBins>> tbinsv;
+    std::vector<std::array<int, 3 * kBins>> tcntv;
+    if (T > 1) {
+      pbbv.resize(T), pcbv.resize(T), tbinsv.resize(T), tcntv.resize(T);
+    }
+    Box* pbb = T > 1 ? pbbv.data() : pbb1;
+    Box* pcb = T > 1 ? pcbv.data() : pcb1;
+    std::array<Box, 3 * kBins>* tbins = T > 1 ? tbinsv.data() : tbins1;
+    std::array<int, 3 * kBins>* tcnt = T > 1 ? tcntv.data() : tcnt1;
+    par(T, nd.first, nd.count, [&](int t, int lo, int hi) {
+      Box bb, cb;
+      for (int i = lo; i < hi; ++i) {
+        bb.grow(pb[idx[i]]);
+        cb.grow_pt(&cen[3 * (size_t)idx[i]]);
+      }
+      pbb[t] = bb;
+      pcb[t] = cb;
+    });
     Box bb, cb;
-    for (int i = nd.first; i < nd.first + nd.count; ++i) {
-      bb.grow(pb[idx[i]]);
-      cb.grow_pt(&cen[3 * (size_t)idx[i]]);
+    for (int t = 0; t < T; ++t) {
+      bb.grow(pbb[t]);
+      cb.grow(pcb[t]);
     }
     nd.box = bb;
-    s.bvh_depth = std::max(s.bvh_depth, nd.depth);
-    if (nd.count <= 1) continue;
+    if (nd.count <= 1) return false;
 
     // binned SAH over all three axes
+    float kinv[3];
+    for (int a = 0; a < 3; ++a) {
+      const float ext = cb.mx[a] - cb.mn[a];
+      kinv[a] = ext > 0 ? kBins / ext : 0.0f;
+    }
+    par(T, nd.first, nd.count, [&](int t, int lo, int hi) {
+      auto& bins = tbins[t];
+      auto& cnt = tcnt[t];
+      cnt.fill(0);
+      for (int i = lo; i < hi; ++i) {
+        const int p = idx[i];
+        for (int a = 0; a < 3; ++a) {
+          if (!(kinv[a] > 0)) continue;
+          int b = (int)((cen[3 * (size_t)p + a] - cb.mn[a]) * kinv[a]);
+          b = std::min(std::max(b, 0), kBins - 1);
+          cnt[a * kBins + b]++;
+          bins[a * kBins + b].grow(pb[p]);
+        }
+      }
+    });
     double best_cost = INFINITY;
     int best_axis = -1, best_split = -1;
     for (int a = 0; a < 3; ++a) {
-      float ext = cb.mx[a] - cb.mn[a];
-      if (!(ext > 0)) continue;
+      if (!(kinv[a] > 0)) continue;
       Box bins[kBins];
       int cnt[kBins] = {0};
-      float k = kBins / ext;
-      for (int i = nd.first; i < nd.first + nd.count; ++i) {
-        int b = (int)((cen[3 * (size_t)idx[i] + a] - cb.mn[a]) * k);
-        b = std::min(std::max(b, 0), kBins - 1);
-        cnt[b]++;
-        bins[b].grow(pb[idx[i]]);
-      }
+      for (int t = 0; t < T; ++t)
+        for (int b = 0; b < kBins; ++b) {
+          bins[b].grow(tbins[t][a * kBins + b]);
+          cnt[b] += tcnt[t][a * kBins + b];
+        }
       double left_area[kBins];
       int left_cnt[kBins];
       Box acc;
@@ -158,8 +221,7 @@ int build_bvh(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi
     double leaf_cost = kCostIsect * nd.count;
     int mid;
     if (best_axis >= 0 && !(nd.count <= kLeafTarget && leaf_cost <= split_cost)) {
-      float ext = cb.mx[best_axis] - cb.mn[best_axis];
-      float k = kBins / ext;
+      const float k = kinv[best_axis];
       auto it = std::partition(idx.begin() + nd.first, idx.begin() + nd.first + nd.count, [&](int p) {
         int b = (int)((cen[3 * (size_t)p + best_axis] - cb.mn[best_axis]) * k);
         b = std::min(std::max(b, 0), kBins - 1);
@@ -167,10 +229,10 @@ int build_bvh(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi
       });
       mid = (int)(it - idx.begin());
     } else if (nd.count <= kLeafTarget) {
-      continue;  // leaf
+      return false;  // leaf
     } else {
       // no usable SAH split (coincident centroids): median split by index
-      if (nd.count <= MAX_LEAF && best_axis < 0) continue;
+      if (nd.count <= MAX_LEAF && best_axis < 0) return false;
       int a = 0;
       float e = -1;
       for (int q = 0; q < 3; ++q)
@@ -183,20 +245,107 @@ int build_bvh(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi
                        [&](int p, int q) { return cen[3 * (size_t)p + a] < cen[3 * (size_t)q + a]; });
     }
     if (mid == nd.first || mid == nd.first + nd.count) mid = nd.first + nd.count / 2;
-    TmpNode L, R;
+    L = TmpNode();
+    R = TmpNode();
     L.first = nd.first;
     L.count = mid - nd.first;
     R.first = mid;
     R.count = nd.first + nd.count - mid;
     L.depth = R.depth = nd.depth + 1;
-    int li = (int)tn.size();
-    tn.push_back(L);
-    tn.push_back(R);
-    tn[ni].left = li;
-    tn[ni].right = li + 1;
-    work.push_back(li + 1);
-    work.push_back(li);
+    return true;
+  };
+  // depth-first build of the subtree under tn_local[0] (one thread)
+  auto build_sub = [&](std::vector<TmpNode>& tl) {
+    std::vector<int> work = {0};
+    while (!work.empty()) {
+      const int ni = work.back();
+      work.pop_back();
+      TmpNode L, R;
+      TmpNode nd = tl[ni];
+      const bool sp = split_node(nd, 1, L, R);
+      tl[ni].box = nd.box;
+      if (!sp) continue;
+      const int li = (int)tl.size();
+      tl.push_back(L);
+      tl.push_back(R);
+      tl[ni].left = li;
+      tl[ni].right = li + 1;
+      work.push_back(li + 1);
+      work.push_back(li);
+    }
+  };
+
+  std::vector<TmpNode> tn;
+  tn.reserve(2 * (size_t)n / kLeafTarget + 16);
+  tn.push_back(TmpNode());
+  tn[0].first = 0;
+  tn[0].count = n;
+  // top of the tree: large nodes one at a time with threaded loops; subtrees
+  // below kSub prims are deferred and built in parallel, one per thread
+  const int kSub = threads > 1 ? std::max(4096, n / (8 * threads)) : n + 1;
+  std::vector<int> deferred;
+  {
+    std::vector<int> work = {0};
+    while (!work.empty()) {
+      const int ni = work.back();
+      work.pop_back();
+      if (tn[ni].count < kSub) {
+        deferred.push_back(ni);
+        continue;
+      }
+      TmpNode L, R;
+      TmpNode nd = tn[ni];
+      const int T = std::min(threads, std::max(1, nd.count / 16384));
+      const bool sp = split_node(nd, T, L, R);
+      tn[ni].box = nd.box;
+      if (!sp) continue;
+      const int li = (int)tn.size();
+      tn.push_back(L);
+      tn.push_back(R);
+      tn[ni].left = li;
+      tn[ni].right = li + 1;
+      work.push_back(li + 1);
+      work.push_back(li);
+    }
   }
+  lap("top levels");
+  if (!deferred.empty()) {
+    std::vector<std::vector<TmpNode>> sub(deferred.size());
+    std::atomic<size_t> next{0};
+    auto worker = [&] {
+      for (size_t k; (k = next.fetch_add(1)) < deferred.size();) {
+        sub[k].reserve(2 * (size_t)tn[deferred[k]].count / kLeafTarget + 4);
+        sub[k].push_back(tn[deferred[k]]);
+        build_sub(sub[k]);
+      }
+    };
+    std::vector<std::thread> th;
+    const int T = std::min<int>(threads, (int)deferred.size());
+    for (int t = 1; t < T; ++t) th.emplace_back(worker);
+    worker();
+    for (auto& x : th) x.join();
+    // splice the subtrees in deferred order (the output order is BFS anyway)
+    for (size_t k = 0; k < deferred.size(); ++k) {
+      const std::vector<TmpNode>& v = sub[k];
+      const int base = (int)tn.size() - 1;  // local index i >= 1 -> base + i
+      TmpNode root = v[0];
+      if (root.left >= 0) {
+        root.left += base;
+        root.right += base;
+      }
+      tn[deferred[k]] = root;
+      for (size_t i = 1; i < v.size(); ++i) {
+        TmpNode x = v[i];
+        if (x.left >= 0) {
+          x.left += base;
+          x.right += base;
+        }
+        tn.push_back(x);
+      }
+    }
+  }
+  for (const auto& x : tn) s.bvh_depth = std::max(s.bvh_depth, x.depth);
+  lap("subtrees");
 
   // permuted refs + bounds
   s.refs.resize(n);
@@ -307,6 +456,7 @@ int build_bvh(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi
     }
   }
   s.root4 = 0;
+  lap("numbering + BVH4");
   return RT_OK;
 }
 

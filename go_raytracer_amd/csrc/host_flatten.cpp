@@ -18,6 +18,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <functional>
 
 #include "rt_internal.h"
@@ -456,8 +457,13 @@ int flatten_scene(const Tree& t, int world, int lights, HostScene& out) {
     return set_error(RT_ERR_INVALID, "rt_scene_create: bad world handle %d", world);
   if (lights >= (int)t.nodes.size())
     return set_error(RT_ERR_INVALID, "rt_scene_create: bad lights handle %d", lights);
+  const bool timing = getenv("RT_TIMING") != nullptr;
+  auto t0 = std::chrono::steady_clock::now();
   Flattener f(t, out);
   int rc = f.walk(world, Xf{}, 1, 0);
+  if (timing)
+    fprintf(stderr, "[rt] flatten walk %.3f s\n",
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
   if (rc) return rc;
   if (lights >= 0) {
     rc = f.walk_lights(lights, 1, 0, 1.0, 0);
@@ -499,7 +505,12 @@ int flatten_scene(const Tree& t, int world, int lights, HostScene& out) {
     out.perlins.push_back(d);
   }
   // keep prim bounds for export, in the BVH's final ref order (set by build_bvh)
-  return build_bvh(out, f.lo, f.hi, f.world_refs);
+  t0 = std::chrono::steady_clock::now();
+  rc = build_bvh(out, f.lo, f.hi, f.world_refs);
+  if (timing)
+    fprintf(stderr, "[rt] build_bvh %.3f s\n",
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+  return rc;
 }
 
 }  // namespace rt

@@ -34,9 +34,9 @@ using sv = std::string_view;
 // ----------------------------------------------------------------- strings
 // unicode.IsSpace over UTF-8 (strings.TrimSpace / strings.Fields): returns the
 // byte length of the space rune at p, 0 if p does not start one.
-int space_len(const char* p, const char* e) {
+inline int space_len(const char* p, const char* e) {
   unsigned char c = (unsigned char)*p;
-  if (c == ' ' || (c >= '\t' && c <= '\r')) return 1;
+  if (c < 0x80) return (c == ' ' || (c >= '\t' && c <= '\r')) ? 1 : 0;
   if (c == 0xC2 && p + 1 < e) {
     unsigned char d = (unsigned char)p[1];
     return (d == 0x85 || d == 0xA0) ? 2 : 0;  // U+0085 NEL, U+00A0 NBSP
@@ -56,6 +56,10 @@ sv trim_space(sv s) {
   const char* b = s.data();
   const char* e = b + s.size();
   for (int n; b < e && (n = space_len(b, e)) > 0;) b += n;
+  // ASCII tail (the common case): strip backwards
+  const char* t = e;
+  while (t > b && (unsigned char)t[-1] < 0x80 && space_len(t - 1, e)) --t;
+  if (t == b || (unsigned char)t[-1] < 0x80) return sv(b, t - b);
   // trailing: scan forward remembering the end of the last non-space rune
   const char* last = b;
   for (const char* p = b; p < e;) {
@@ -82,6 +86,15 @@ void fields(sv s, std::vector<sv>& out) {
     while (p < e && space_len(p, e) == 0) ++p;
     out.emplace_back(b, p - b);
   }
+}
+
+// the first field of a trimmed, non-empty line (strings.Fields(line)[0])
+inline sv first_field(sv s) {
+  const char* b = s.data();
+  const char* e = b + s.size();
+  const char* p = b;
+  while (p < e && space_len(p, e) == 0) ++p;
+  return sv(b, p - b);
 }
 
 void split_slash(sv s, std::vector<sv>& out) {  // strings.Split(s, "/")
@@ -227,12 +240,67 @@ bool go_parse_float(sv s, double* out) {
   }
   if (underscores && !underscore_ok(s.substr(0, i))) return false;
   if (i != s.size()) return false;
-  // the grammar matched: both Go and strtod round correctly
-  std::string clean;
-  clean.reserve(s.size());
+  // the grammar matched.  Clinger's fast path when it is exact: a decimal
+  // mantissa M <= 2^53 and |exp10| <= 22 give M * 10^e (or M / 10^-e) with ONE
+  // rounding, i.e. the correctly rounded value Go returns; else strtod (also
+  // correctly rounded).  Typical OBJ coordinates (<= 15 digits) take the fast path.
+  if (!hex && !underscores) {
+    static const double kP10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,
+                                    1e8,  1e9,  1e10, 1e11, 1e12, 1e13, 1e14, 1e15,
+                                    1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+    size_t k = 0;
+    const bool neg = s[0] == '-';
+    if (s[0] == '+' || s[0] == '-') ++k;
+    uint64_t m = 0;
+    int nd = 0, e10 = 0;
+    bool ok = true, dot = false;
+    for (; k < s.size(); ++k) {
+      const char c = s[k];
+      if (c == '.') {
+        dot = true;
+        continue;
+      }
+      if (c < '0' || c > '9') break;
+      if (m == 0 && c == '0') {  // leading zeros carry no digits
+        if (dot) --e10;
+        continue;
+      }
+      if (++nd > 16) {
+        ok = false;
+        break;
+      }
+      m = m * 10 + (uint64_t)(c - '0');
+      if (dot) --e10;
+    }
+    if (ok && k < s.size()) {  // exponent
+      ++k;
+      bool eneg = false;
+      if (s[k] == '+' || s[k] == '-') eneg = s[k++] == '-';
+      int ev = 0;
+      for (; k < s.size() && ev < 10000; ++k) ev = ev * 10 + (s[k] - '0');
+      if (k < s.size()) ok = false;
+      e10 += eneg ? -ev : ev;
+    }
+    if (ok && m <= (1ull << 53) && e10 >= -22 && e10 <= 22) {
+      double v = (double)m;
+      v = e10 >= 0 ? v * kP10[e10] : v / kP10[-e10];
+      *out = neg ? -v : v;
+      return true;
+    }
+  }
+  // strtod needs a NUL-terminated copy without underscores; tokens are short
+  char buf[128];
+  std::string big;
+  char* q = buf;
+  if (s.size() >= sizeof buf) {
+    big.resize(s.size() + 1);
+    q = &big[0];
+  }
+  size_t nq = 0;
   for (char c : s)
-    if (c != '_') clean.push_back(c);
-  double v = strtod(clean.c_str(), nullptr);
+    if (c != '_') q[nq++] = c;
+  q[nq] = 0;
+  double v = strtod(q, nullptr);
   *out = v;
   return !isinf(v);  // overflow: ErrRange with ±Inf (underflow is not an error)
 }
@@ -568,6 +636,7 @@ int rt_load_obj_memory(rt_tree* t, const char* obj_text, size_t obj_len, const c
     while (lines.next(line)) {
       sv s = trim_space(line);
       if (s.empty() || s[0] == '#') continue;
+      if (first_field(s) != "mtllib") continue;
       fields(s, p);
       if (p.empty()) continue;
       if (p[0] == "mtllib" && p.size() >= 2) {
@@ -609,6 +678,8 @@ int rt_load_obj_memory(rt_tree* t, const char* obj_text, size_t obj_len, const c
     while (lines.next(line)) {
       sv s = trim_space(line);
       if (s.empty() || s[0] == '#') continue;
+      const sv head = first_field(s);
+      if (head != "v" && head != "vt") continue;  // the only keys this pass reads
       fields(s, p);
       if (p.empty()) continue;
       if (p[0] == "vt") {
@@ -669,6 +740,8 @@ int rt_load_obj_memory(rt_tree* t, const char* obj_text, size_t obj_len, const c
     while (lines.next(line)) {
       sv s = trim_space(line);
       if (s.empty() || s[0] == '#') continue;
+      const sv head = first_field(s);
+      if (head != "vn" && head != "f" && head != "usemtl") continue;
       fields(s, p);
       if (p.empty()) continue;
       sv k = p[0];

@@ -365,7 +365,8 @@ void knot_point(double s, double* p) {
   p[2] = r * sin(P * s) * 0.18;
 }
 
-// The substitute as OBJ text ("OBJ units", before LoadObjWithOptions' scale):
+// The substitute as OBJ text ("OBJ units", before LoadObjWithOptions' scale),
+// 9 significant digits like a typical exported mesh:
 // nu*nv vertices with vertex normals and one quad face per grid cell, which the
 // loader fans into the triangles (a,b,c), (a,c,d) (objLoader.go:396-397).
 std::string substitute_dragon_obj(int nu, int nv) {
@@ -398,14 +399,14 @@ std::string substitute_dragon_obj(int nu, int nv) {
       double rr = a * (1.0 + 0.18 * sin(7 * phi) * sin(23 * s));
       double dir[3];
       for (int k = 0; k < 3; ++k) dir[k] = cos(phi) * N[k] + sin(phi) * B[k];
-      snprintf(line, sizeof line, "v %.17g %.17g %.17g\n", c0[0] + rr * dir[0],
+      snprintf(line, sizeof line, "v %.9g %.9g %.9g\n", c0[0] + rr * dir[0],
                c0[1] + rr * dir[1], c0[2] + rr * dir[2]);
       out += line;
       memcpy(&norms[3 * ((size_t)i * nv + j)], dir, sizeof dir);
     }
   }
   for (size_t v = 0; v < norms.size(); v += 3) {
-    snprintf(line, sizeof line, "vn %.17g %.17g %.17g\n", norms[v], norms[v + 1], norms[v + 2]);
+    snprintf(line, sizeof line, "vn %.9g %.9g %.9g\n", norms[v], norms[v + 1], norms[v + 2]);
     out += line;
   }
   auto id = [&](int i, int j) { return (long)(i % nu) * nv + (j % nv) + 1; };

@@ -288,3 +288,34 @@ def test_loaded_model_flattens(rt, mixed):
     with rt.Scene(t, world, lights) as sc:
         i = sc.info()
     assert i["n_triangles"] >= 16 and i["n_lights"] == 2
+
+
+def test_c_parse_float_is_correctly_rounded(rt):
+    """The loader's fast path (Clinger: mantissa <= 2^53, |exp10| <= 22) and its
+    strtod fallback both return the correctly rounded double, like Go's ParseFloat:
+    compared bit for bit with Python's float() on random decimal strings."""
+    rng = np.random.default_rng(5)
+    toks = []
+    for _ in range(3000):
+        nd = int(rng.integers(1, 20))
+        digits = "".join(str(int(d)) for d in rng.integers(0, 10, nd))
+        dot = int(rng.integers(0, nd + 1))
+        s = digits[:dot] + "." + digits[dot:] if rng.random() < 0.8 else digits
+        if s in (".", ""):
+            s = "0"
+        if rng.random() < 0.3:
+            s += "e" + str(int(rng.integers(-30, 30)))
+        if rng.random() < 0.5:
+            s = "-" + s
+        toks.append(s)
+    n = len(toks) // 3
+    text = "".join(f"v {a} {b} {c}\n" for a, b, c in zip(toks[0::3], toks[1::3], toks[2::3]))
+    text += "".join(f"f {i} {i + 1} {i + 2}\n" for i in range(1, n - 1, 3))
+    t = rt.Tree()
+    model, lights = t.LoadObjWithOptions(None, rt.LoadObjOptions(Debug=False, Center=False),
+                                         obj_text=text.encode())
+    tris, _ = tree_triangles(t, model, lights)
+    got = [x for tr in tris for x in tr[0]]
+    want = [float(x) for x in toks[:len(got)]]
+    assert len(got) >= 2900
+    assert [struct.pack("<d", x) for x in got] == [struct.pack("<d", x) for x in want]

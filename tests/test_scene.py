@@ -134,3 +134,17 @@ def test_demo_scene_numbers(rt):
     assert rt.lib().rt_demo_scene_name(6, C.byref(name)) == 0 and name.value == b"cornell"
     assert rt.lib().rt_demo_scene_name(8, C.byref(name)) == 0 and name.value == b"model"
     assert rt.lib().rt_demo_scene_name(9, C.byref(name)) < 0
+
+
+def test_bvh_build_is_thread_count_invariant(rt, monkeypatch):
+    """The SAH build runs its top levels with threaded loops and the subtrees in
+    parallel (host_bvh.cpp); min/max box growth and integer bin counts make the
+    tree bit-identical for any thread count."""
+    out = {}
+    for th in ("1", "3", "8"):
+        monkeypatch.setenv("RT_THREADS", th)
+        t, cam, w, l = rt.demo_scene("model:256x64")
+        with rt.Scene(t, w, l) as sc:
+            nodes, refs, root, bounds = sc.export_bvh()
+        out[th] = (nodes.tobytes(), refs.tobytes(), int(root), bounds.tobytes())
+    assert out["1"] == out["3"] == out["8"]

@@ -1,0 +1,6 @@
+set -o pipefail
+O=gpurun_out
+timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_v22.log 2>&1 || { tail -30 $O/pytest_v22.log; exit 1; }
+tail -1 $O/pytest_v22.log
+bash tools/ab_configs.sh $O/ab_configs_v22.jsonl && cut -c1-110 $O/ab_configs_v22.jsonl
+timeout -k 10 200 python3 tools/share_probe.py 2>&1 | grep '^{'
