@@ -76,6 +76,11 @@ V = {
         "        trav_brute<FT, !LDS>(P.sc, lnodes, s.o, s.d, s.time, 0.001f, tr);\n"
         "        tr.best.t = fminf(tr.best.t, t2.best.t + 0.0f * tr.best.t); }")],
 }
+V["dbl_trav4"] = [("go_raytracer_amd/csrc/rt_render.hip",
+    "        trav_steps<LDS, FT, TREE == 4>(P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, tr,\n                                       P.step_budget);",
+    "      { Trav t2 = tr; trav_steps<LDS, FT, TREE == 4>(P.sc, lnodes, recs_lds, ts, s.o, s.d * 1.0000001f, s.time, 0.001f, t2, P.step_budget);\n"
+    "        trav_steps<LDS, FT, TREE == 4>(P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, tr, P.step_budget);\n"
+    "        tr.best.t = fminf(tr.best.t, t2.best.t + 0.0f * tr.best.t); }")]
 names = sys.argv[1:] or list(V)
 for name in names:
     d = f"/tmp/abl/{name}"
