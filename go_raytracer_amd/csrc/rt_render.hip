@@ -168,6 +168,9 @@ __global__ __launch_bounds__(256) void k_init(Params P) {
 // FT = compiled-in scene features (rt_device.h), chosen per scene by pick_fused.
 // Waves per SIMD by feature set: the lean sets fit more waves in the register
 // file (VGPRs <= 512 / waves) and in LDS (24 KB static + the scene cache).
+#ifndef MESH_WAVES
+#define MESH_WAVES 4
+#endif
 #ifndef FT_TEX_WAVES
 #define FT_TEX_WAVES 4
 #endif
@@ -180,7 +183,7 @@ constexpr int fused_waves(uint32_t ft, int tree = 4) {
   return (tree == 0 && ft == 0u) ? kBruteWaves  // 7 measured within noise of 6, 8 -3 %
          : ft == 0u ? 6
          : ft == FT_MEDIA ? 4
-         : ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? 4
+         : ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? MESH_WAVES
          : ft == (FT_SPHERE | FT_METAL | FT_DIEL | FT_MEDIA | FT_IMAGE | FT_NOISE) ? FT_TEX_WAVES
                                                                                   : 3;
 }
