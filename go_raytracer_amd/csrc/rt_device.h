@@ -136,6 +136,8 @@ struct DevScene {
   const uint8_t* texels;
   const DevImage* images;
   const DevPerlin* perlins;
+  int32_t brute_ax[3];  // record loop (TREE 0): axis-aligned pairs per normal axis, after
+  int32_t _pad_ax;      // the general pairs (host-grouped; rt_path.h brute_axis)
 };
 
 }  // namespace rt

@@ -380,27 +380,67 @@ RT_D v2f pfma(v2f a, v2f b, v2f c) { return __builtin_elementwise_fma(a, b, c); 
 RT_D bool unit_ab(float a, float b) {
   return max(__float_as_uint(a), __float_as_uint(b)) <= 0x3F800000u;
 }
+// one record pair's loop fields (7 x 16 B) from the LDS cache or the scalar cache
+template <bool SMEM>
+RT_D void load_pair(const DevScene& sc, const F4* lrec, int p, v4f r[7]) {
+  if (SMEM) {
+    typedef __attribute__((address_space(4))) const v4f cst_v4;
+    const cst_v4* q = (const cst_v4*)sc.leafprims + 8 * __builtin_amdgcn_readfirstlane(p);
+#pragma unroll
+    for (int e = 0; e < 7; ++e) r[e] = q[e];
+  } else {
+    const lds_v4* q = (const lds_v4*)lrec + 8 * p;
+#pragma unroll
+    for (int e = 0; e < 7; ++e) r[e] = q[e];
+  }
+}
+// component I of Q, A, B for both records (floats 8-13, 14-19, 20-25 of the pair)
+template <int I> RT_D v2f pair_q(const v4f* r) { return I == 0 ? r[2].xy : I == 1 ? r[2].zw : r[3].xy; }
+template <int I> RT_D v2f pair_a(const v4f* r) { return I == 0 ? r[3].zw : I == 1 ? r[4].xy : r[4].zw; }
+template <int I> RT_D v2f pair_b(const v4f* r) { return I == 0 ? r[5].xy : I == 1 ? r[5].zw : r[6].xy; }
+// Axis-aligned pairs (unit normal +-e_AX, A_AX = B_AX = 0; grouped by the host after
+// the general pairs).  With n = +-e_AX the general test's n.d is +-d_AX and n.o is
+// +-o_AX, and the zero components of n, A and B add exact zeros, so t = (D' - o_AX)
+// * rcp(d_AX) with D' = D / n_AX (stored by the host) and alpha, beta over the two
+// in-plane axes are the general test's values bit for bit: 10 packed ops per pair
+// instead of 20, and one rcp per ray and axis instead of two per pair.
+template <int AX, bool SMEM>
+RT_D void brute_axis(const DevScene& sc, const F4* lrec, int p0, int p1, const v2f* O,
+                     const v2f* Dv, float tmin, float& best, uint32_t& bk) {
+  constexpr int B0 = AX == 0 ? 1 : 0, B1 = AX == 2 ? 1 : 2;  // in-plane axes, ascending
+  const float da = Dv[AX].x;
+  const float ia = fabsf(da) >= 1e-8f ? rcp(da) : __builtin_nanf("");  // |n.d| < 1e-8: no hit
+  const v2f inv = {ia, ia};
+  for (int p = p0; p < p1; ++p) {
+    v4f r[7];
+    load_pair<SMEM>(sc, lrec, p, r);
+    const uint32_t k0 = __float_as_uint(r[6].z), k1 = __float_as_uint(r[6].w);
+    const v2f t = (r[1].zw - O[AX]) * inv;
+    const v2f pb = pfma(Dv[B0], t, O[B0]) - pair_q<B0>(r);
+    const v2f pc = pfma(Dv[B1], t, O[B1]) - pair_q<B1>(r);
+    const v2f a = pfma(pc, pair_a<B1>(r), pb * pair_a<B0>(r));
+    const v2f b = pfma(pc, pair_b<B1>(r), pb * pair_b<B0>(r));
+    const bool c0 = t.x >= tmin && unit_ab(a.x, b.x) && t.x <= best;
+    best = c0 ? t.x : best;
+    bk = c0 ? k0 : bk;
+    const bool c1 = t.y >= tmin && unit_ab(a.y, b.y) && t.y <= best;
+    best = c1 ? t.y : best;
+    bk = c1 ? k1 : bk;
+  }
+}
 template <uint32_t FT, bool SMEM>
 RT_D void trav_brute(const DevScene& sc, const F4* lrec, f3 o, f3 d, float time, float tmin,
                      Trav& tr) {
   static_assert(!HAS(FT_SPHERE | FT_TRI), "record loop: quad-only feature sets");
-  const int np = sc.n_refs >> 1;  // pairs (the host pads to an even count)
+  const int nax = sc.brute_ax[0], nay = sc.brute_ax[1], naz = sc.brute_ax[2];
+  const int ng = (sc.n_refs >> 1) - nax - nay - naz;  // general pairs first (even count)
   const v2f ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
   const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z};
   float best = tr.best.t;
   uint32_t bk = 0xFFFFFFFFu;
-  for (int p = 0; p < np; ++p) {
+  for (int p = 0; p < ng; ++p) {
     v4f r[7];
-    if (SMEM) {
-      typedef __attribute__((address_space(4))) const v4f cst_v4;
-      const cst_v4* q = (const cst_v4*)sc.leafprims + 8 * __builtin_amdgcn_readfirstlane(p);
-#pragma unroll
-      for (int e = 0; e < 7; ++e) r[e] = q[e];
-    } else {
-      const lds_v4* q = (const lds_v4*)lrec + 8 * p;
-#pragma unroll
-      for (int e = 0; e < 7; ++e) r[e] = q[e];
-    }
+    load_pair<SMEM>(sc, lrec, p, r);
     // record indices 2p, 2p+1 as stored data: the select takes them from a VGPR
     // (a loop-counter SGPR would need a v_mov first: one constant-bus read per op)
     const uint32_t k0 = __float_as_uint(r[6].z), k1 = __float_as_uint(r[6].w);
@@ -420,6 +460,10 @@ RT_D void trav_brute(const DevScene& sc, const F4* lrec, f3 o, f3 d, float time,
     best = c1 ? t.y : best;
     bk = c1 ? k1 : bk;
   }
+  const v2f O[3] = {ox, oy, oz}, Dv[3] = {dx, dy, dz};
+  brute_axis<0, SMEM>(sc, lrec, ng, ng + nax, O, Dv, tmin, best, bk);
+  brute_axis<1, SMEM>(sc, lrec, ng + nax, ng + nax + nay, O, Dv, tmin, best, bk);
+  brute_axis<2, SMEM>(sc, lrec, ng + nax + nay, ng + nax + nay + naz, O, Dv, tmin, best, bk);
   if (bk != 0xFFFFFFFFu) {
     // the winner's fields (pair bk/2, half bk&1): Q at floats 8/10/12, A at
     // 14/16/18, B at 20/22/24, ref at 28 (+ half)

@@ -301,6 +301,7 @@ struct DeviceScene {
   DevScene d{};                 // nodes = BVH4
   const F4* nodes2 = nullptr;   // BVH2 of the same leaves (tiny scenes)
   const F4* brute_pairs = nullptr;  // quad records in pairs, largest first (record loop)
+  size_t brute_slots = 0;           // records in brute_pairs, pads included (even)
   uint32_t root2 = PRIM_NONE;
   int32_t n_nodes2 = 0;
   ~DeviceScene() {
@@ -485,19 +486,64 @@ static int ensure_scene(Scene* s, int device) {
     };
     std::stable_sort(ord.begin(), ord.end(),
                      [&](size_t a, size_t b) { return area(h.refs[a]) > area(h.refs[b]); });
+    // Axis-aligned quads (unit normal +-e_a, A_a = B_a = 0 exactly: Cornell's walls,
+    // floor, ceiling and box tops) go in per-axis pair groups after the general
+    // pairs; the loop tests them with the in-plane terms only, bit-identical to the
+    // general test (rt_path.h brute_axis).  An odd record of a group joins the
+    // general list.  RT_BRUTE_AXIS=0 keeps every record general (A/B).
+    const bool use_axis = env_int("RT_BRUTE_AXIS", 1) != 0;
+    auto axis_of = [&](size_t i) -> int {
+      const F4* r = &recs[4 * i];
+      if (!use_axis || (h.refs[i] >> 30) != PRIM_QUAD) return -1;
+      const float n[3] = {r[1].x, r[1].y, r[1].z}, A[3] = {r[2].x, r[2].y, r[2].z},
+                  B[3] = {r[3].x, r[3].y, r[3].z};
+      for (int a = 0; a < 3; ++a) {
+        const int b = (a + 1) % 3, c = (a + 2) % 3;
+        if ((n[a] == 1.0f || n[a] == -1.0f) && n[b] == 0.0f && n[c] == 0.0f && A[a] == 0.0f &&
+            B[a] == 0.0f)
+          return a;
+      }
+      return -1;
+    };
+    std::vector<size_t> grp[4];  // 0-2: axis groups, 3: general
+    for (size_t i : ord) {
+      const int a = axis_of(i);
+      grp[a < 0 ? 3 : a].push_back(i);
+    }
+    for (int a = 0; a < 3; ++a)
+      if (grp[a].size() & 1) {
+        grp[3].push_back(grp[a].back());  // the group's smallest record
+        grp[a].pop_back();
+      }
+    std::stable_sort(grp[3].begin(), grp[3].end(),
+                     [&](size_t a, size_t b) { return area(h.refs[a]) > area(h.refs[b]); });
+    std::vector<long> slots;  // record per slot in loop order, -1 = pad
+    for (size_t i : grp[3]) slots.push_back((long)i);
+    if (slots.size() & 1) slots.push_back(-1);
+    const size_t n_general = slots.size();
+    for (int a = 0; a < 3; ++a) {
+      for (size_t i : grp[a]) slots.push_back((long)i);
+      d.brute_ax[a] = (int32_t)(grp[a].size() / 2);
+    }
+    if (slots.empty()) slots.assign(2, -1);
     // pair layout (rt_device.h): records 2p, 2p+1 interleaved field by field
-    const size_t n_even = (ord.size() + 1) & ~(size_t)1;
-    std::vector<F4> pairs(std::max<size_t>(4 * n_even, 8), F4{0, 0, 0, 0});  // pad: n = 0, never hit
-    for (size_t i = 0; i < ord.size(); ++i) {
-      const F4* r = &recs[4 * ord[i]];  // Q|ref, n|D, A, B
+    std::vector<F4> pairs(4 * slots.size(), F4{0, 0, 0, 0});  // pad: n = 0, never hit
+    for (size_t i = 0; i < slots.size(); ++i) {
+      if (slots[i] < 0) continue;
+      const F4* r = &recs[4 * (size_t)slots[i]];  // Q|ref, n|D, A, B
       float* f = (float*)&pairs[8 * (i / 2)] + (i & 1);
       float kb;
       const uint32_t k = (uint32_t)i;
       memcpy(&kb, &k, 4);
-      const float v[15] = {r[1].x, r[1].y, r[1].z, r[1].w, r[0].x, r[0].y, r[0].z, r[2].x,
+      // axis records: D / n_a (= +-D exactly) in the D slot, so t = (D' - o_a) / d_a
+      const int a = i >= n_general ? axis_of((size_t)slots[i]) : -1;
+      const float na = a == 0 ? r[1].x : a == 1 ? r[1].y : r[1].z;
+      const float Dp = a < 0 ? r[1].w : na * r[1].w;
+      const float v[15] = {r[1].x, r[1].y, r[1].z, Dp,     r[0].x, r[0].y, r[0].z, r[2].x,
                            r[2].y, r[2].z, r[3].x, r[3].y, r[3].z, kb,     r[0].w};
       for (int e = 0; e < 15; ++e) f[2 * e] = v[e];
     }
+    s->dev->brute_slots = slots.size();
     if ((rc = upload(s->dev, pairs, &s->dev->brute_pairs)) != RT_OK) return rc;
   }
   UP(h.media, media);
@@ -670,7 +716,7 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
       (env_tree == 4 || (!s->h.nodes.empty() && s->h.nodes.size() / 4 + n_refs <= slots_for(2))))
     tree = env_tree;  // A/B override
   const size_t lds_slots = slots_for(tree);
-  const size_t brute_slots = (n_refs + 1) & ~(size_t)1;  // record-loop pairs, 2 x 64 B each
+  const size_t brute_slots = s->dev->brute_slots;  // record-loop pairs, 2 x 64 B each
   const int smem_env = env_int("RT_BRUTE_SMEM", -1);
   const bool brute_smem =
       tree == 0 && (smem_env >= 0 ? smem_env != 0 : brute_slots > lds_slots);

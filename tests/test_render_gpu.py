@@ -90,3 +90,19 @@ def test_kernel_selection(rt, gpu, name, width, lean, width_tree, lds):
         assert st["tree_width"] == width_tree
     if lds is not None:
         assert st["lds_scene"] == lds
+
+
+def test_axis_record_groups_match_general_test(rt, gpu, monkeypatch):
+    """The record loop's axis-aligned groups (rt_path.h brute_axis) compute the
+    general quad test's t, alpha and beta bit for bit: the Cornell box renders the
+    same image with the grouping switched off (RT_BRUTE_AXIS=0)."""
+    t, cam, w, l = rt.demo_scene("cornell")
+    cam.Width, cam.SamplesPerPixel = 96, 64
+    imgs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("RT_BRUTE_AXIS", flag)
+        with rt.Scene(t, w, l) as sc:
+            img, st = sc.render(cam, seed=4, chunk=8)
+        assert st["tree_width"] == 0
+        imgs.append(img)
+    assert np.array_equal(imgs[0], imgs[1])
