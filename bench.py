@@ -1,17 +1,28 @@
 #!/usr/bin/env python3
-"""bench.py — Msamples/s of the HIP path tracer on BASELINE.json's config C2.
+"""bench.py — Msamples/s of the HIP path tracer on BASELINE.json's configs.
 
-Workload (a "step"): one full render of the Cornell box (main.go:278-320) at
-800x800 with 1024 samples per pixel (32x32 strata, camera.go:211-213), MaxDepth
-50 = 655.36 M camera samples, rows interleaved across ranks (row r -> rank
-r % N) and gathered to every rank with one RCCL all_gather over xGMI.  The scene
-is uploaded to HBM during warmup; the timed region holds only render + gather.
+Headline workload (a "step"): one full render of the Cornell box (configs[1] = C2,
+main.go:278-320) at 800x800 with 1024 samples per pixel (32x32 strata,
+camera.go:211-213), MaxDepth 50 = 655.36 M camera samples, rows interleaved across
+ranks (row r -> rank r % N, camera.go:119-122) and gathered with one RCCL
+all_gather over xGMI.  The scene is uploaded to HBM during warmup; the timed region
+holds only render + gather.
+
+After the headline, `extra_configs` times BASELINE configs C3 (book1), C4 (book2)
+and C5 (model) the same way (row shares on every rank, barrier + max over ranks),
+each with its own roofline, so every GPU config has a measured line.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 
-Prints one JSON line (rank 0).  See DESIGN.md "Measurement" for the roofline
-model (SURVEY.md §8(d) algorithmic bytes) and the CPU baseline definition.
+Prints one JSON line (rank 0).  Roofline (DESIGN.md "Roofline"): the fused kernel
+keeps path state in registers and LDS, so what binds it is VALU instruction
+issue, not HBM.  `roofline` reports the counter-backed VALU-issue fraction
+(SQ_INSTS_VALU per launch from a rocprofv3 --pmc pass, profiles/traffic.json,
+divided by the live kernel time and the chip's 1228.8 G wave-instructions/s),
+next to the counter-backed HBM fraction (FETCH_SIZE x2 + WRITE_SIZE per launch)
+and SURVEY.md §8(d)'s wavefront-state model (segments x 164 B ...), which is a
+throughput index for a pipeline this kernel does not run.
 """
 import argparse
 import json
@@ -23,6 +34,9 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+# VALU issue: 256 CUs x 4 SIMDs x 2.4 GHz, one wave64 VALU instruction per SIMD per
+# 2 cycles (SIMD-32, MI355X_MICROARCH.md "Execution model") = 1228.8 G wave-instr/s
+PEAK_VALU_GIPS = 256 * 4 * 2.4 / 2
 # SURVEY.md §8(d) / BASELINE.md algorithmic bytes: Bytes = 164*S + 48*N + 15*W*H
 B_PER_SEG = 164
 B_PER_SAMPLE = 48
@@ -30,6 +44,11 @@ B_PER_PIXEL = 15
 EXTEND_B_PER_SEG = 44        # the extend kernel's share: ray 28 read + hit 16 written
 SHADE_B_PER_SEG = 120        # shade's share: hit 16 + ray 28 + key 8 read, ray 28 + key 8 +
 #                              weight 12 written, queue 8, fold re-read 12
+
+# BASELINE.json configs timed after the headline (name, scene, width, spp, steps)
+EXTRA = [("C3", "book1", 1200, 512, 3),   # main.go:19-91, aspect 1.5 -> 1200x800, 484 spp
+         ("C4", "book2", 800, 4096, 1),   # main.go:94-174
+         ("C5", "model", 1920, 1024, 2)]  # main.go:371-409, 1M-triangle substitute mesh
 
 
 def parse():
@@ -43,32 +62,109 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--mode", default="auto", choices=["auto", "fused", "wavefront"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra-configs", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline work")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"),
-                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py)")
+                    help="PMC counters per launch (tools/pmc_traffic.py)")
     return ap.parse_args()
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(tree, world, lights, cam, target_s):
-    """The oracle (C++ fp64 restatement of the Go CPU path) on a bounded,
-    row-interleaved sample of the same image at full spp."""
+    """The oracle (C++ fp64 restatement of the Go CPU path, camera.go:112-153) on
+    bounded row-interleaved samples of the same image at full spp: with the box's
+    CPU share (16 threads: the GPU box's allotment, OMP_NUM_THREADS) and with one
+    thread (the reference's -N=1, syncRenderer camera.go:135-153).  The whole
+    host's rate is stated as the single-thread rate x nproc (ideal scaling, an
+    upper bound for the Go path).  Also times configs[0] (C1, quads 400x400x64,
+    -N=1, main.go:220-247) in full."""
     from oracle import pyoracle
-    threads = min(16, os.cpu_count() or 1)
+    import go_raytracer_amd as rt
+    nproc = os.cpu_count() or 1
+    threads = min(16, nproc)
     d = cam.derived()
-    # calibrate on one row, then pick a row stride that gives ~target_s of work
-    _, st = pyoracle.render(tree, world, lights, cam, seed=1, threads=threads, rank=0,
-                            nranks=d.height, max_rows=1)
-    rate = st["samples"] / max(st["seconds"], 1e-6)
-    rows_wanted = max(1, int(target_s * rate / (d.width * d.spp_sqrt ** 2)))
-    stride = max(1, d.height // rows_wanted)
-    _, st = pyoracle.render(tree, world, lights, cam, seed=1, threads=threads, rank=0,
-                            nranks=stride)
-    rows = len(range(0, d.height, stride))
-    return {"value": st["samples"] / st["seconds"] / 1e6, "unit": "Msamples/s",
-            "cores": threads, "kind": "port",
+    px_row = d.width * d.spp_sqrt ** 2
+
+    def sample(nthreads, seconds):
+        _, st = pyoracle.render(tree, world, lights, cam, seed=1, threads=nthreads, rank=0,
+                                nranks=d.height, max_rows=1)
+        rate = st["samples"] / max(st["seconds"], 1e-6)
+        rows_wanted = max(1, int(seconds * rate / px_row))
+        stride = max(1, d.height // rows_wanted)
+        _, st = pyoracle.render(tree, world, lights, cam, seed=1, threads=nthreads, rank=0,
+                                nranks=stride)
+        return st, stride, len(range(0, d.height, stride))
+
+    st, stride, rows = sample(threads, target_s)
+    st1, stride1, rows1 = sample(1, target_s / 3)
+    v16 = st["samples"] / st["seconds"] / 1e6
+    v1 = st1["samples"] / st1["seconds"] / 1e6
+    # configs[0]: C1 quads 400x400, 64 spp, one thread, the whole image
+    tq, camq, wq, lq = rt.demo_scene("quads")
+    camq.Width, camq.SamplesPerPixel = 400, 64
+    _, stq = pyoracle.render(tq, wq, lq, camq, seed=1, threads=1)
+    return {"value": v16, "unit": "Msamples/s", "cores": threads, "kind": "port",
             "sample": f"every {stride}th row ({rows} rows x {d.width} px) of the same image at "
                       f"full {d.spp_sqrt ** 2} spp, {st['samples']} samples in "
-                      f"{st['seconds']:.1f} s, {threads} threads"}
+                      f"{st['seconds']:.1f} s, {threads} threads (the GPU box's CPU share)",
+            "single_thread": {"value": v1, "unit": "Msamples/s", "cores": 1,
+                              "sample": f"every {stride1}th row ({rows1} rows), "
+                                        f"{st1['samples']} samples in {st1['seconds']:.1f} s"},
+            "host": {"nproc": nproc, "cpu_model": cpu_model(),
+                     "extrapolated_all_cores_Msamples_s": round(v1 * nproc, 2),
+                     "note": "single-thread rate x nproc: ideal scaling over every host "
+                             "thread (not run: the box allots 16)"},
+            "c1_plumbing": {"config": "configs[0]: quads 400x400x64, -N=1 (main.go:220-247)",
+                            "samples": stq["samples"], "seconds": round(stq["seconds"], 3),
+                            "Msamples_s": round(stq["samples"] / stq["seconds"] / 1e6, 3),
+                            "segments_per_sample": round(stq["segments"] / stq["samples"], 4)}}
+
+
+def load_traffic(path):
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
+
+
+def roofline(db, key, kernel, ms, seg, smp, pix):
+    """Rooflines of one launch of `kernel` (ms = live average launch time)."""
+    model_bytes = seg * B_PER_SEG + smp * B_PER_SAMPLE + pix * B_PER_PIXEL
+    model_gbs = model_bytes / max(ms, 1e-9) / 1e6
+    pmc = db.get(key, {}).get(kernel, {})
+    valu = pmc.get("valu_insts_per_launch")
+    hbm = pmc.get("hbm_bytes_per_launch")
+    r = {"bound": "issue", "kernel": kernel, "achieved": None, "peak": PEAK_VALU_GIPS,
+         "unit": "G VALU wave-instr/s", "frac": None, "traffic": hbm}
+    if valu:
+        a = valu / ms / 1e6
+        r.update(achieved=round(a, 2), frac=round(a / PEAK_VALU_GIPS, 4),
+                 valu_insts_per_launch=valu)
+    if hbm:
+        g = hbm / ms / 1e6
+        r["hbm_counter"] = {"achieved": round(g, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                            "frac": round(g / PEAK_HBM_GBS, 4),
+                            "bytes_per_launch": hbm, "source": "FETCH_SIZE*2 + WRITE_SIZE"}
+    r["hbm_model"] = {"achieved": round(model_gbs, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                      "frac": round(model_gbs / PEAK_HBM_GBS, 4),
+                      "bytes_per_launch": model_bytes,
+                      "model": "164*segments + 48*samples + 15*pixels (SURVEY §8d wavefront "
+                               "state; a throughput index: the fused kernel keeps this state "
+                               "in registers/LDS and does not move these bytes)"}
+    if pmc.get("_source"):
+        r["pmc_source"] = pmc["_source"]
+    return r
 
 
 def main():
@@ -88,7 +184,49 @@ def main():
     dev = torch.device("cuda", local_rank)
     if world_size > 1:
         dist.init_process_group("nccl", device_id=dev)
+    stream = torch.cuda.current_stream(dev)
+    db = load_traffic(args.traffic)
 
+    def timed_renders(scene, cam, steps, warmup, buf, gathered, profile=True):
+        """warmup + `steps` renders of this rank's share (+ all_gather), barrier and
+        synchronize around the timed region; returns (max elapsed, per-step stats)."""
+        def step(prof):
+            st = scene.render_device(cam, buf.data_ptr(), seed=args.seed, device=local_rank,
+                                     rank=rank, nranks=world_size, profile=prof,
+                                     stream=stream.cuda_stream, mode=args.mode)
+            if world_size > 1:
+                dist.all_gather_into_tensor(gathered, buf)
+            return st
+        t_first = None
+        for i in range(warmup):
+            t0 = time.perf_counter()
+            step(False)
+            if i == 0:
+                torch.cuda.synchronize()
+                t_first = time.perf_counter() - t0
+        torch.cuda.synchronize()
+        if world_size > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        stats = [step(profile) for _ in range(steps)]
+        torch.cuda.synchronize()
+        if world_size > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        if world_size > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t.item(), stats, t_first
+
+    def buffers(d):
+        rows_per = (d.height + world_size - 1) // world_size
+        buf = torch.zeros((rows_per, d.width, 3), dtype=torch.float32, device=dev)
+        gathered = torch.zeros((world_size * rows_per, d.width, 3), dtype=torch.float32,
+                               device=dev)
+        return buf, gathered
+
+    # ------------------------------------------------------------ headline (C2)
     t_build0 = time.perf_counter()
     tree, cam, w, l = rt.demo_scene(args.scene)
     cam.Width = args.width
@@ -97,108 +235,44 @@ def main():
         cam.AspectRatio = 1.5  # 1200x800 needs aspect 1.5
     d = cam.derived()
     H, W = d.height, d.width
-    rows_per = (H + world_size - 1) // world_size
-    rows_mine = len(range(rank, H, world_size))
-    buf = torch.zeros((rows_per, W, 3), dtype=torch.float32, device=dev)
-    gathered = torch.zeros((world_size * rows_per, W, 3), dtype=torch.float32, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    buf, gathered = buffers(d)
     scene = rt.Scene(tree, w, l)
     t_build = time.perf_counter() - t_build0
-
-    def step(profile):
-        st = scene.render_device(cam, buf.data_ptr(), seed=args.seed, device=local_rank,
-                                 rank=rank, nranks=world_size, profile=profile,
-                                 stream=stream.cuda_stream, mode=args.mode)
-        if world_size > 1:
-            dist.all_gather_into_tensor(gathered, buf)
-        return st
-
-    t_first, t_first0 = None, time.perf_counter()
-    for i in range(args.warmup):
-        step(False)
-        if i == 0:
-            torch.cuda.synchronize()
-            t_first = time.perf_counter() - t_first0
-    torch.cuda.synchronize()
-    if world_size > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    stats = [step(True) for _ in range(args.steps)]
-    torch.cuda.synchronize()
-    if world_size > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    elapsed, stats, t_first = timed_renders(scene, cam, args.steps, args.warmup, buf, gathered)
     samples = torch.tensor([sum(s["samples"] for s in stats)], dtype=torch.float64, device=dev)
     if world_size > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(samples, op=dist.ReduceOp.SUM)
-    elapsed = t.item()
     total_samples = samples.item()
-
+    line = None
     if rank == 0:
         seg = sum(s["segments"] for s in stats)
         smp = sum(s["samples"] for s in stats)
         pix = sum(s["rows"] for s in stats) * W
-        ms_ext = sum(s["ms_extend"] for s in stats)
-        ms_sh = sum(s["ms_shade"] for s in stats)
-        ms_fu = sum(s["ms_fused"] for s in stats)
-        n_ext = sum(s["n_extend_launches"] for s in stats)
-        n_sh = sum(s["n_shade_launches"] for s in stats)
         mode = {1: "wavefront", 2: "fused"}[stats[0]["mode"]]
-        total_bytes = seg * B_PER_SEG + smp * B_PER_SAMPLE + pix * B_PER_PIXEL
+        key = f"{args.scene}:{W}x{H}x{d.spp_sqrt ** 2}"
         if mode == "fused":
-            # one persistent launch per step does all of the path's work
-            kernels = {"k_fused": {"launches": len(stats), "avg_ms": ms_fu / len(stats),
-                                   "alg_bytes_per_launch": total_bytes / len(stats),
-                                   "achieved_GBs": total_bytes / max(ms_fu, 1e-9) / 1e6}}
-        else:
-            ext_bytes = seg * EXTEND_B_PER_SEG
-            sh_bytes = seg * SHADE_B_PER_SEG + smp * B_PER_SAMPLE + pix * B_PER_PIXEL
-            kernels = {
-                "k_extend": {"launches": n_ext, "avg_ms": ms_ext / max(n_ext, 1),
-                             "alg_bytes_per_launch": ext_bytes / max(n_ext, 1),
-                             "achieved_GBs": ext_bytes / max(ms_ext, 1e-9) / 1e6},
-                "k_shade": {"launches": n_sh, "avg_ms": ms_sh / max(n_sh, 1),
-                            "alg_bytes_per_launch": sh_bytes / max(n_sh, 1),
-                            "achieved_GBs": sh_bytes / max(ms_sh, 1e-9) / 1e6},
-            }
-        dom = max(kernels, key=lambda k: kernels[k]["avg_ms"] * kernels[k]["launches"])
-        traffic = None
-        if os.path.exists(args.traffic):
-            try:
-                with open(args.traffic) as f:
-                    tr = json.load(f)
-                key = f"{args.scene}:{W}x{H}x{d.spp_sqrt ** 2}"
-                if key in tr and dom in tr[key]:
-                    traffic = tr[key][dom]["hbm_bytes_per_launch"]
-            except (OSError, ValueError, KeyError):
-                traffic = None
-        k = kernels[dom]
-        roofline = {"bound": "hbm", "kernel": dom, "achieved": round(k["achieved_GBs"], 2),
-                    "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                    "frac": round(k["achieved_GBs"] / PEAK_HBM_GBS, 5), "traffic": traffic,
-                    "alg_bytes_model": "164*segments + 48*samples + 15*pixels (SURVEY §8d)",
-                    "kernels": {n: {kk: round(v, 4) for kk, v in kv.items()}
-                                for n, kv in kernels.items()}}
-        # end-to-end wall clock around the render (the metric's "+ wall-clock"):
-        # scene build on the host (demo scene + flatten + BVH), the first step
-        # (scene upload + render), and the P3 text of the image built on the GPU
+            ms = sum(s["ms_fused"] for s in stats) / len(stats)
+            roof = roofline(db, key, "k_fused", ms, seg / len(stats), smp / len(stats),
+                            pix / len(stats))
+            roof["launches"] = len(stats)
+            roof["avg_ms"] = round(ms, 4)
+        else:  # the wavefront pair: the model's bytes per kernel (cross-check path)
+            n_ext = sum(s["n_extend_launches"] for s in stats)
+            ms_ext = sum(s["ms_extend"] for s in stats)
+            ms_sh = sum(s["ms_shade"] for s in stats)
+            roof = {"bound": "hbm", "kernel": "k_extend+k_shade", "unit": "GB/s",
+                    "peak": PEAK_HBM_GBS, "traffic": None,
+                    "achieved": round((seg * (EXTEND_B_PER_SEG + SHADE_B_PER_SEG) + smp *
+                                       B_PER_SAMPLE + pix * B_PER_PIXEL) /
+                                      max(ms_ext + ms_sh, 1e-9) / 1e6, 2),
+                    "launches": n_ext}
+            roof["frac"] = round(roof["achieved"] / PEAK_HBM_GBS, 4)
         from go_raytracer_amd import shard
         torch.cuda.synchronize()
         t_ppm0 = time.perf_counter()
         ppm = rt.format_ppm_device(buf if world_size == 1 else
                                    shard.assemble(gathered, H, world_size))
         t_ppm = time.perf_counter() - t_ppm0
-        wall = {"scene_build_s": round(t_build, 3),
-                "first_step_s": None if t_first is None else round(t_first, 3),
-                "render_step_s": round(elapsed / args.steps, 4),
-                "ppm_on_device_s": round(t_ppm, 4), "ppm_bytes": len(ppm)}
-        cpu = None
-        if world_size == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(tree, w, l, cam, args.cpu_seconds)
         value = total_samples / elapsed / 1e6
         line = {
             "metric": "Msamples/sec (pixels×spp/s) + wall-clock, Cornell Box 800×800×1024spp",
@@ -206,20 +280,85 @@ def main():
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": f"{args.scene} {W}x{H} {d.spp_sqrt ** 2}spp maxdepth {d.max_depth} "
-                                   f"(BASELINE configs[1], main.go cornellBox)",
+            "config": {"workload": f"{args.scene} {W}x{H} {d.spp_sqrt ** 2}spp maxdepth "
+                                   f"{d.max_depth} (BASELINE configs[1], main.go cornellBox)",
                        "scene": args.scene, "width": W, "height": H, "spp": d.spp_sqrt ** 2,
                        "max_depth": d.max_depth, "parallelism": f"rows%{world_size}",
                        "mode": mode, "path_slots": stats[0]["path_slots"],
-                       "segments_per_sample": round(seg / max(smp, 1), 4)},
-            "roofline": roofline, "cpu_baseline": cpu, "wall_clock": wall,
+                       "chunk_samples": stats[0]["chunk_samples"],
+                       "segments_per_sample": round(seg / max(smp, 1), 4),
+                       "Gsegments_per_s": round(seg / (elapsed * rank_share(world_size)) / 1e9, 3)},
+            "roofline": roof,
+            "wall_clock": {"scene_build_s": round(t_build, 3),
+                           "first_step_s": None if t_first is None else round(t_first, 3),
+                           "render_step_s": round(elapsed / args.steps, 4),
+                           "ppm_on_device_s": round(t_ppm, 4), "ppm_bytes": len(ppm)},
         }
-        if cpu:
-            line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
-        print(json.dumps(line), flush=True)
     scene.close()
+
+    # ------------------------------------------------------- C3, C4, C5 lines
+    extra = {}
+    if not args.no_extra_configs:
+        for name, sname, width, spp, steps in EXTRA:
+            tb0 = time.perf_counter()
+            t2, cam2, w2, l2 = rt.demo_scene(sname)
+            cam2.Width, cam2.SamplesPerPixel = width, spp
+            if sname == "book1":
+                cam2.AspectRatio = 1.5
+            d2 = cam2.derived()
+            b2, g2 = buffers(d2)
+            with rt.Scene(t2, w2, l2) as sc2:
+                spp_keep = cam2.SamplesPerPixel
+                cam2.SamplesPerPixel = 1  # warmup: scene upload + state buffers only
+                timed_renders(sc2, cam2, 0, 1, b2, g2, profile=False)
+                tbuild = time.perf_counter() - tb0
+                cam2.SamplesPerPixel = spp_keep
+                el, st2, _ = timed_renders(sc2, cam2, steps, 0, b2, g2)
+            tot = torch.tensor([sum(s["samples"] for s in st2)], dtype=torch.float64, device=dev)
+            if world_size > 1:
+                dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+            if rank == 0:
+                seg = sum(s["segments"] for s in st2) / steps
+                smp = sum(s["samples"] for s in st2) / steps
+                pix = sum(s["rows"] for s in st2) / steps * d2.width
+                ms = sum(s["ms_fused"] for s in st2) / steps
+                key = f"{sname}:{d2.width}x{d2.height}x{d2.spp_sqrt ** 2}"
+                roof = roofline(db, key, "k_fused", ms, seg, smp, pix)
+                roof["avg_ms"] = round(ms, 4)
+                extra[name] = {
+                    "workload": f"{sname} {d2.width}x{d2.height} {d2.spp_sqrt ** 2}spp maxdepth "
+                                f"{d2.max_depth}",
+                    "value": round(tot.item() / el / 1e6, 3), "unit": "Msamples/s",
+                    "ms_per_step": round(el / steps * 1e3, 3), "steps": steps,
+                    "segments_per_sample": round(seg / max(smp, 1), 4),
+                    "Gsegments_per_s_rank0": round(seg / (ms / 1e3) / 1e9, 3),
+                    "tree_width": st2[0]["tree_width"], "lds_scene": st2[0]["lds_scene"],
+                    "chunk_samples": st2[0]["chunk_samples"],
+                    "scene_setup_s": round(tbuild, 3), "roofline": roof}
+            del b2, g2
+    if rank == 0:
+        if extra:
+            line["extra_configs"] = extra
+        cpu = None
+        if world_size == 1 and not args.no_cpu_baseline:
+            tree, cam, w, l = rt.demo_scene(args.scene)
+            cam.Width, cam.SamplesPerPixel = args.width, args.spp
+            if args.scene == "book1":
+                cam.AspectRatio = 1.5
+            cpu = cpu_baseline(tree, w, l, cam, args.cpu_seconds)
+        line["cpu_baseline"] = cpu
+        if cpu:
+            line["speedup_vs_cpu"] = round(line["value"] / cpu["value"], 1)
+            line["speedup_vs_host_extrapolated"] = round(
+                line["value"] / cpu["host"]["extrapolated_all_cores_Msamples_s"], 1)
+        print(json.dumps(line), flush=True)
     if world_size > 1:
         dist.destroy_process_group()
+
+
+def rank_share(n):
+    """Segments are rank 0's; the rate per rank is seg / elapsed."""
+    return 1.0
 
 
 if __name__ == "__main__":

@@ -36,11 +36,13 @@ class Tree:
         p = C.c_void_p()
         check(lib().rt_tree_create(C.byref(p)))
         self._p = p
+        # bound now: at interpreter shutdown module globals (lib) may already be None
+        self._destroy = lib().rt_tree_destroy
         check(lib().rt_tree_seed(self._p, seed))
 
     def __del__(self):
         if getattr(self, "_p", None):
-            lib().rt_tree_destroy(self._p)
+            self._destroy(self._p)
             self._p = None
 
     @property
@@ -372,11 +374,12 @@ class Scene:
         p = C.c_void_p()
         check(lib().rt_scene_create(tree.ptr, world, lights, C.byref(p)))
         self._p = p
+        self._destroy = lib().rt_scene_destroy  # usable at interpreter shutdown
         self.tree = tree
 
     def close(self):
         if getattr(self, "_p", None):
-            lib().rt_scene_destroy(self._p)
+            self._destroy(self._p)
             self._p = None
 
     __del__ = close
@@ -457,6 +460,22 @@ class Scene:
             res["trace"] = tbuf[tbuf[:, 7] >= 0]
         return out, res
 
+    def render_multi(self, camera, devices, seed=1, path_slots=0, chunk=0, profile=False,
+                     mode="auto"):
+        """The whole image over several devices (rt_render_multi: row r on
+        devices[r % n], peer-copied to devices[0]) -> (float32 [H, W, 3], stats)."""
+        d = camera.derived()
+        out = np.zeros((d.height, d.width, 3), np.float32)
+        st = _multi(self, camera, devices, (out.ctypes.data, False), seed, path_slots, chunk,
+                    profile, mode)
+        return out, st
+
+    def render_multi_device(self, camera, devices, out_ptr, seed=1, path_slots=0, chunk=0,
+                            profile=False, mode="auto"):
+        """rt_render_multi_device: the whole image into a device buffer on devices[0]."""
+        return _multi(self, camera, devices, (out_ptr, True), seed, path_slots, chunk, profile,
+                      mode)
+
     def render_device(self, camera, out_ptr, seed=1, device=0, rank=0, nranks=1, path_slots=0,
                       chunk=0, profile=False, stream=None, mode="auto"):
         """Render into a device buffer (e.g. torch tensor .data_ptr()) on `stream`."""
@@ -466,6 +485,18 @@ class Scene:
         check(lib().rt_render_device(self._p, C.byref(c), C.byref(o), C.c_void_p(out_ptr),
                                      C.byref(st)))
         return {f: getattr(st, f) for f, _ in RtStats._fields_}
+
+
+def _multi(scene, camera, devices, out_ptr, seed, path_slots, chunk, profile, mode):
+    devs = (C.c_int32 * len(devices))(*[int(d) for d in devices])
+    st = RtStats()
+    c = camera.to_c()
+    o = scene._opts(seed, int(devices[0]) if len(devices) else 0, 0, 1, path_slots, chunk,
+                    profile, None, mode)
+    fn = lib().rt_render_multi_device if out_ptr[1] else lib().rt_render_multi
+    check(fn(scene._p, C.byref(c), C.byref(o), devs, len(devices), C.c_void_p(out_ptr[0]),
+             C.byref(st)))
+    return {f: getattr(st, f) for f, _ in RtStats._fields_}
 
 
 def demo_scene(name, seed=1, asset_dir=None):

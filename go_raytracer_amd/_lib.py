@@ -85,6 +85,7 @@ class RtStats(C.Structure):
         ("kernel_features", C.c_int32), ("scene_features", C.c_int32),
         ("tree_width", C.c_int32), ("lds_scene", C.c_int32),
         ("chunk_samples", C.c_int32), ("_pad2", C.c_int32),
+        ("overflow_samples", C.c_uint64),
     ]
 
 
@@ -176,6 +177,11 @@ SIGNATURES = {
                        C.POINTER(RtStats)]),
     "rt_render_device": (_I, [_P, C.POINTER(RtCamera), C.POINTER(RtRenderOpts), C.c_void_p,
                               C.POINTER(RtStats)]),
+    "rt_render_multi": (_I, [_P, C.POINTER(RtCamera), C.POINTER(RtRenderOpts),
+                             C.POINTER(C.c_int32), C.c_int32, C.c_void_p, C.POINTER(RtStats)]),
+    "rt_render_multi_device": (_I, [_P, C.POINTER(RtCamera), C.POINTER(RtRenderOpts),
+                                    C.POINTER(C.c_int32), C.c_int32, C.c_void_p,
+                                    C.POINTER(RtStats)]),
     "rt_quantize": (_I, [C.c_void_p, C.c_int64, C.c_void_p]),
     "rt_format_ppm": (C.c_int64, [C.c_void_p, _I, _I, C.c_void_p, C.c_int64]),
     "rt_progress": (_I, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),

@@ -6,30 +6,72 @@
 using rt::set_error;
 
 namespace rt {
+
+static uint32_t fbits_host(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  return u;
+}
 // Prim types reachable by traversal, shading or light sampling, material kinds
 // and texture kinds present: selects the fused-kernel instantiation.
+// Features of what a render can reach: the world's and lights' prims, the media,
+// the materials of those prims and media, and the textures of those materials
+// (through checker children).  Materials and textures that are built but never
+// placed (book1's perlin orbs, main.go:52-60) do not count, so such a scene runs a
+// leaner kernel.  RT_FEATURES_ALL=1 counts every table entry (A/B).
 uint32_t scene_features(const HostScene& h) {
   uint32_t f = 0;
-  auto prim = [&f](uint32_t ref) {
+  std::vector<char> mat_used(h.mats.size(), 0);
+  auto use_mat = [&](int m) {
+    if (m >= 0 && (size_t)m < mat_used.size()) mat_used[m] = 1;
+  };
+  auto prim = [&](uint32_t ref) {
     if (ref == PRIM_NONE) return;
-    const uint32_t type = ref >> 30;
-    if (type == PRIM_SPHERE) f |= FT_SPHERE;
-    if (type == PRIM_TRI) f |= FT_TRI;
-    if (type == PRIM_MEDIUM) f |= FT_MEDIA;
+    const uint32_t type = ref >> 30, idx = ref & 0x3FFFFFFFu;
+    if (type == PRIM_SPHERE) {
+      f |= FT_SPHERE;
+      if (idx < h.sph_mv.size()) use_mat((int)fbits_host(h.sph_mv[idx].w));
+    } else if (type == PRIM_QUAD) {
+      if (5 * (size_t)idx + 2 < h.quad.size()) use_mat((int)fbits_host(h.quad[5 * (size_t)idx + 2].w));
+    } else if (type == PRIM_TRI) {
+      f |= FT_TRI;
+      if (3 * (size_t)idx < h.tri.size()) use_mat((int)fbits_host(h.tri[3 * (size_t)idx].w));
+    } else {
+      f |= FT_MEDIA;
+    }
   };
   for (uint32_t r : h.refs) prim(r);
   for (uint32_t r : h.medium_refs) prim(r);
   for (const DevLight& l : h.lights) prim(l.ref);
   if (!h.media.empty()) f |= FT_MEDIA;
-  for (const DevMaterial& m : h.mats) {
+  for (const DevMedium& m : h.media) use_mat(m.phase_mat);
+  const char* all = getenv("RT_FEATURES_ALL");
+  const bool every = all && *all && atoi(all) != 0;
+  std::vector<char> tex_used(h.texs.size(), 0);
+  std::vector<int> st;
+  for (size_t i = 0; i < h.mats.size(); ++i) {
+    if (!mat_used[i] && !every) continue;
+    const DevMaterial& m = h.mats[i];
     if (m.kind == RT_MAT_METAL) f |= FT_METAL;
     if (m.kind == RT_MAT_DIELECTRIC) f |= FT_DIEL;
     if (m.kind == RT_MAT_ISOTROPIC) f |= FT_MEDIA;
+    if (m.kind != RT_MAT_METAL && m.kind != RT_MAT_DIELECTRIC && m.tex >= 0) st.push_back(m.tex);
   }
-  for (const DevTexture& t : h.texs) {
-    if (t.kind == RT_TEX_CHECKER) f |= FT_CHECKER;
-    if (t.kind == RT_TEX_IMAGE) f |= FT_IMAGE;
-    if (t.kind == RT_TEX_NOISE) f |= FT_NOISE;
+  if (every)
+    for (size_t i = 0; i < h.texs.size(); ++i) st.push_back((int)i);
+  while (!st.empty()) {
+    const int t = st.back();
+    st.pop_back();
+    if (t < 0 || (size_t)t >= h.texs.size() || tex_used[t]) continue;
+    tex_used[t] = 1;
+    const DevTexture& T = h.texs[t];
+    if (T.kind == RT_TEX_CHECKER) {
+      f |= FT_CHECKER;
+      st.push_back(T.a);
+      st.push_back(T.b);
+    }
+    if (T.kind == RT_TEX_IMAGE) f |= FT_IMAGE;
+    if (T.kind == RT_TEX_NOISE) f |= FT_NOISE;
   }
   return f;
 }

@@ -3,6 +3,7 @@
 #include <stdint.h>
 
 #include <atomic>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -80,11 +81,23 @@ struct Progress {
   std::vector<uint64_t> cum;    // samples complete when event i has fired
 };
 
+// Render buffers of one (device, slot): slot 0 serves rt_render / rt_render_device,
+// slots 1..n the shares of rt_render_multi (so {0, 0, 0} gets three of them).  The
+// mutex is held for the whole render: one render in flight per (scene, device, slot).
+struct SlotState {
+  std::mutex mu;
+  RenderState* st = nullptr;
+};
+
 struct Scene {
   HostScene h;
-  int device = -1;
-  DeviceScene* dev = nullptr;     // uploaded lazily by rt_render
-  RenderState* state = nullptr;   // wavefront buffers, reused across renders
+  std::mutex mu;                                    // guards the maps (not the renders)
+  std::map<int, DeviceScene*> devs;                 // per device ordinal, uploaded lazily
+  std::map<std::pair<int, int>, SlotState*> slots;  // per (device, slot)
+  std::mutex multi_mu;                              // one rt_render_multi at a time
+  void* multi_buf = nullptr;                        // gather + image buffer on the first device
+  size_t multi_bytes = 0;
+  int multi_dev = -1;
   Progress prog;
 };
 

@@ -13,6 +13,7 @@ namespace rt {
 
 constexpr float kPi = 3.14159265358979323846f;
 constexpr float kInf = __builtin_huge_valf();
+constexpr float kInvPi = 0.318309886183790671538f;
 
 struct f3 {
   float x, y, z;

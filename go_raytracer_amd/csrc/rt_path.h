@@ -24,8 +24,9 @@ enum { OUT_DEAD = 0, OUT_ALIVE = 1, OUT_NEED_CHUNK = 2 };
 struct Counters {
   unsigned long long segments;
   unsigned long long pushes;
+  unsigned long long overflow;  // samples whose channel left the fixed-point range (add_sample)
   uint32_t chunk_head;
-  uint32_t _pad[13];
+  uint32_t _pad[11];
   uint32_t cnt[kMaxIt][kXcd];  // per-XCD queue lengths entering iteration i
 };
 
@@ -67,12 +68,13 @@ struct Params {
   uint2* path; // chunk, packed(j:12 | vertex:8 | nstack:8 | flags:4)
   F4* pend;    // pending clamp-vertex weight (top of the weight stack)
   F4* pre;     // camera-side product of specular attenuations
-  F4* acc;     // chunk accumulator
   F4* stack;   // [vertex][slot] clamp-vertex weights spilled to HBM
   uint32_t* queue[2];  // each kXcd segments of P entries
   Counters* ctr;
-  unsigned long long* accum;  // 3 planes x npix, fixed point 2^-32
-  uint32_t* pflags;           // per pixel NaN (bits 0-2) / Inf (bits 3-5)
+  unsigned long long* accum;  // 3 planes x npix: per-sample fixed point 2^-32, summed exactly
+  double* side;               // 3 planes x npix: samples outside the fixed-point range (fp64)
+  float vlim;                 // fixed-point range per sample: |v| < 2^31 / ss (no int64 wrap)
+  uint32_t* pflags;           // per pixel NaN (bits 0-2) / +Inf (bits 3-5) / -Inf (bits 6-8)
   uint32_t* ostack;            // traversal-stack overflow [kStack - kShortStackMin][stack_cols]
   uint32_t stack_cols;         // = launched threads of the traversal kernel
   F4* trace;                  // debug path trace (3 F4 per vertex) or null
@@ -750,22 +752,82 @@ RT_D f3 lights_random(const DevScene& sc, f3 origin, const rt_u32x4& r) {
   return p - origin;
 }
 
-RT_D void flush_chunk(const Params& P, uint32_t chunk, f3 acc) {
-  const uint32_t lp = chunk - fdiv(chunk, P.fd_npix) * P.npix;
-  const float c[3] = {acc.x, acc.y, acc.z};
+// ---------------------------------------------------------- pixel sums -----
+// pixelColor += rayColor(...) (camera.go:97-101) for every sample, in fixed point:
+// each sample's channel becomes floor(v * 2^32) and the pixel sums are int64, so
+// the sum is exact and independent of how samples are grouped into chunks, which
+// lane or kernel renders them, and how rows are split over ranks (bitwise the same
+// image for any chunk size, schedule, strategy and GPU count).  |v| < vlim = 2^31/ss
+// keeps the ss-sample sum inside int64; a finite sample outside that range (never
+// in the BASELINE scenes) is added in fp64 to a side plane and counted
+// (Counters::overflow, rt_stats.overflow_samples); NaN and +-Inf set pixel flags
+// with the reference's sum semantics (NaN, or +Inf and -Inf, give NaN).
+RT_D uint32_t local_pixel(const Params& P, uint32_t chunk) {
+  return chunk - fdiv(chunk, P.fd_npix) * P.npix;
+}
+// floor(v * 2^32) for |v| < 2^31: the integer part in the high word, the fraction
+// (exact: v - floor(v) loses no bits, and * 2^32 only moves the exponent) in the low
+RT_D unsigned long long to_fixed(float v) {
+  const float hi = floorf(v);
+  const uint32_t lo = (uint32_t)((v - hi) * 4294967296.0f);
+  return ((unsigned long long)(uint32_t)(int32_t)hi << 32) | lo;
+}
+// a sample with a channel outside the fixed-point range or non-finite (rare): every
+// channel goes straight to the pixel (fixed-point channels included: the integer sum
+// does not care where it is added)
+RT_D void add_sample_rare(const Params& P, uint32_t lp, float x, float y, float z) {
+  const float c[3] = {x, y, z};
   for (int ch = 0; ch < 3; ++ch) {
-    float v = c[ch];
-    if (isnan(v)) {
+    const float v = c[ch];
+    if (fabsf(v) < P.vlim) {
+      atomicAdd(&P.accum[(size_t)ch * P.npix + lp], to_fixed(v));
+    } else if (isnan(v)) {
       atomicOr(&P.pflags[lp], 1u << ch);
     } else if (isinf(v)) {
-      atomicOr(&P.pflags[lp], 8u << ch);
+      atomicOr(&P.pflags[lp], (v > 0.0f ? 8u : 64u) << ch);
     } else {
-      float cl = fminf(fmaxf(v, -2147483648.0f), 2147483520.0f);
-      long long fx = (long long)(cl * 4294967296.0f);
-      atomicAdd(&P.accum[(size_t)ch * P.npix + lp], (unsigned long long)fx);
+      atomicAdd(&P.side[(size_t)ch * P.npix + lp], (double)v);
+      atomicAdd(&P.ctr->overflow, 1ull);
     }
   }
 }
+typedef __attribute__((address_space(3))) unsigned long long lds_u64;
+// Per-lane chunk sums: the fused kernel keeps them in an LDS column (3 x u64 per
+// lane, [channel][thread]; ds_add_u64, no registers held across the path) and
+// flushes them to the pixel with one global atomic per channel when the chunk
+// ends; the wavefront kernels (lds == null) add every sample to the pixel.
+struct SampleAcc {
+  unsigned long long* lds;  // &lacc[0][threadIdx.x], stride 256, or null
+  RT_D void add(const Params& P, uint32_t chunk, f3 L) const {
+    const bool fixed = fabsf(L.x) < P.vlim && fabsf(L.y) < P.vlim && fabsf(L.z) < P.vlim;
+    if (!fixed) {
+      add_sample_rare(P, local_pixel(P, chunk), L.x, L.y, L.z);
+      return;
+    }
+    const unsigned long long fx = to_fixed(L.x), fy = to_fixed(L.y), fz = to_fixed(L.z);
+    if (lds) {
+      __atomic_fetch_add((lds_u64*)lds, fx, __ATOMIC_RELAXED);
+      __atomic_fetch_add((lds_u64*)lds + 256, fy, __ATOMIC_RELAXED);
+      __atomic_fetch_add((lds_u64*)lds + 512, fz, __ATOMIC_RELAXED);
+    } else {
+      const uint32_t lp = local_pixel(P, chunk);
+      atomicAdd(&P.accum[lp], fx);
+      atomicAdd(&P.accum[(size_t)P.npix + lp], fy);
+      atomicAdd(&P.accum[2 * (size_t)P.npix + lp], fz);
+    }
+  }
+  RT_D void flush(const Params& P, uint32_t chunk) const {
+    if (!lds) return;
+    const uint32_t lp = local_pixel(P, chunk);
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      lds_u64* q = (lds_u64*)lds + ch * 256;
+      const unsigned long long s = *q;
+      *q = 0ull;
+      if (s) atomicAdd(&P.accum[(size_t)ch * P.npix + lp], s);
+    }
+  }
+};
 
 // ------------------------------------------------------------- path state --
 // One path.  In the fused kernel every field lives in registers; in the
@@ -776,7 +838,7 @@ struct Path {
   float time;
   uint32_t chunk, j, k, nst, flags;
   uint32_t gpix, s0;  // global pixel and first sample of the chunk (chunk_ids, cached)
-  f3 pend, pre, acc;
+  f3 pend, pre;
   uint32_t segs, pushes;  // per-lane statistics (fused kernel)
 };
 
@@ -797,15 +859,6 @@ template <bool SOA>
 RT_D void set_pre(const Params& P, uint32_t slot, Path& s, f3 v) {
   if (SOA) P.pre[slot] = {v.x, v.y, v.z, 0.0f};
   else s.pre = v;
-}
-template <bool SOA>
-RT_D f3 get_acc(const Params& P, uint32_t slot, const Path& s) {
-  return SOA ? xyz(P.acc[slot]) : s.acc;
-}
-template <bool SOA>
-RT_D void set_acc(const Params& P, uint32_t slot, Path& s, f3 v) {
-  if (SOA) P.acc[slot] = {v.x, v.y, v.z, 0.0f};
-  else s.acc = v;
 }
 
 // Clamp-weight stack: entries below nlds in an LDS column (fused kernel, one
@@ -904,7 +957,8 @@ RT_D void start_sample(const Params& P, uint32_t slot, Path& s, uint32_t chunk, 
 // One vertex of rayColor (camera.go:293-331) given its closest hit.
 // Returns OUT_ALIVE (continue with s.o/s.d), or OUT_NEED_CHUNK (chunk flushed).
 template <bool SOA, uint32_t FT>
-RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const WStack& ws) {
+RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const WStack& ws,
+                    const SampleAcc& sa) {
   const DevScene& sc = P.sc;
   const f3 o = s.o, d = s.d;
   const float time = s.time;
@@ -1032,9 +1086,9 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
           spdf = 1.0f / (4.0f * kPi);
         } else {
           f3 ud = unit(ndir);
-          bsdf_pdf = fmaxf(0.0f, dot(ud, b.w) / kPi);
+          bsdf_pdf = fmaxf(0.0f, dot(ud, b.w) * kInvPi);  // 1 ulp of /pi, no division sequence
           float ct = dot(n, ud);
-          spdf = ct < 0.0f ? 0.0f : ct / kPi;
+          spdf = ct < 0.0f ? 0.0f : ct * kInvPi;
         }
         float pdf = 0.5f * lights_pdf<FT>(sc, p, ndir) + 0.5f * bsdf_pdf;
         weight = (att * spdf) * rcp(pdf);
@@ -1080,17 +1134,15 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
   } else {
     L = mk3(0, 0, 0);
   }
-  f3 acc = L;
-  if (s.j > 0) acc = get_acc<SOA>(P, slot, s) + L;
+  sa.add(P, s.chunk, L);
   const uint32_t count = min(P.K, P.ss - s.s0);  // chunk_ids().count
   if (s.j + 1 < count) {
-    set_acc<SOA>(P, slot, s, acc);
     if (!have_rcam)  // a miss, or the depth limit: the camera draw is made here
       rcam = rt_rng_draw(P.seed, s.gpix, s.s0 + s.j + 1, RT_STREAM_CAMERA);
     next_sample<SOA>(P, slot, s, s.j + 1, rcam);
     return OUT_ALIVE;
   }
-  flush_chunk(P, s.chunk, acc);
+  sa.flush(P, s.chunk);
   return OUT_NEED_CHUNK;
 }
 

@@ -23,6 +23,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "rt_internal.h"
@@ -118,7 +120,8 @@ __global__ __launch_bounds__(256) void k_shade(Params P, int it) {
     const F4 hv = P.hit[slot];
     const Hit h = {hv.x, hv.y, hv.z, fbits(hv.w)};
     const WStack ws = {nullptr, 0};  // the weight stack outlives the launch: HBM only
-    int out = shade_core<true, FT_ALL>(P, slot, s, h, ws);
+    const SampleAcc sa = {nullptr};  // every sample straight to its pixel
+    int out = shade_core<true, FT_ALL>(P, slot, s, h, ws, sa);
     if (out == OUT_NEED_CHUNK) {
       // static work split: slot s renders chunks s, s+P, s+2P, ... (no atomics)
       const uint32_t c = s.chunk + P.P;
@@ -188,28 +191,48 @@ constexpr int fused_waves(uint32_t ft, int tree = 4) {
                                                                                   : 3;
 }
 // LDS clamp-weight entries (12 B each): 6 (C2 +1 %, C3 +2.5 % over 3-4), 4 for the
-// mesh set, whose specular paths rarely push weights (C5 -1.5 % with 6)
-constexpr int fused_wlds(uint32_t ft) {
-  return ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? 4 : kLdsWMax;
+// mesh set, whose specular paths rarely push weights (C5 -1.5 % with 6), and 4 for
+// the lean set's tree kernels (their stack + sums must fit 6 waves/SIMD)
+#ifndef MESH_WLDS
+#define MESH_WLDS 4
+#endif
+#ifndef MESH_SHORT
+#define MESH_SHORT kShortStack
+#endif
+#ifndef ALL_WLDS
+#define ALL_WLDS 4  // 6 pushed the C3-size trees out of the 3-wave LDS budget
+#endif
+constexpr int fused_wlds(uint32_t ft, int tree = 4) {
+  return ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? MESH_WLDS
+         : (ft == 0u && tree != 0)                                  ? 4
+         : ft == FT_ALL                                             ? ALL_WLDS
+                                                                    : kLdsWMax;
 }
 // short traversal stack: none for the record loop, 6 entries for the lean set
 // (tiny trees; its LDS budget at 6 waves/SIMD), 12 elsewhere; deeper ones in HBM
 constexpr int fused_short(uint32_t ft, int tree = 4) {
-  return tree == 0 ? 0 : ft == 0u ? kShortStackMin : kShortStack;
+  return tree == 0                                                    ? 0
+         : ft == 0u                                                   ? kShortStackMin
+         : ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? MESH_SHORT
+                                                                      : kShortStack;
 }
+// + 24 B per lane of chunk sums (SampleAcc)
 constexpr unsigned fused_static_lds(uint32_t ft, int tree = 4) {
-  return (unsigned)(fused_short(ft, tree) * 4 + fused_wlds(ft) * 12) * 256u;
+  return (unsigned)(fused_short(ft, tree) * 4 + fused_wlds(ft, tree) * 12 + 24) * 256u;
 }
 // TREE: 4 = BVH4, 2 = BVH2, 0 = no tree (every record tested, tiny scenes)
 template <bool LDS, uint32_t FT, int TREE>
 __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) {
   extern __shared__ F4 lnodes[];  // LDS scene cache, sized at launch (scene_lds_bytes)
   __shared__ uint32_t lstack[(fused_short(FT, TREE) > 0 ? fused_short(FT, TREE) : 1) * 256];
-  __shared__ float lw[3 * fused_wlds(FT) * 256];
+  __shared__ float lw[3 * fused_wlds(FT, TREE) * 256];
+  __shared__ unsigned long long lacc[3 * 256];  // per-lane chunk sums (SampleAcc)
+  for (int ch = 0; ch < 3; ++ch) lacc[ch * 256 + threadIdx.x] = 0ull;
   const bool recs_lds = LDS && stage_nodes(P, lnodes, TREE == 4 ? 8 : 4);
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;  // weight-stack column
   const TravStack ts = {&lstack[threadIdx.x], P.ostack + slot, P.stack_cols, fused_short(FT, TREE)};
-  const WStack ws = {&lw[threadIdx.x], fused_wlds(FT)};
+  const WStack ws = {&lw[threadIdx.x], fused_wlds(FT, TREE)};
+  const SampleAcc sa = {&lacc[threadIdx.x]};
   Path s;
   s.segs = 0;
   s.pushes = 0;
@@ -246,7 +269,7 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
         Hit best = tr.best;
         finish_hit<FT>(P, s, best);
         ++s.segs;
-        if (shade_core<false, FT>(P, slot, s, best, ws) == OUT_NEED_CHUNK) has = false;
+        if (shade_core<false, FT>(P, slot, s, best, ws, sa) == OUT_NEED_CHUNK) has = false;
         else trav_init(P.sc, s.d, tr);
       }
     }
@@ -274,14 +297,17 @@ __global__ __launch_bounds__(256) void k_resolve(Params P, float* out, double sc
   if (lp >= P.npix) return;
   const uint32_t f = P.pflags[lp];
   for (int ch = 0; ch < 3; ++ch) {
+    const bool nan = (f & (1u << ch)) != 0, pinf = (f & (8u << ch)) != 0,
+               ninf = (f & (64u << ch)) != 0;
     float v;
-    if (f & (1u << ch)) {
+    if (nan || (pinf && ninf)) {  // Inf + -Inf = NaN, as in the fp64 sum
       v = __builtin_nanf("");
-    } else if (f & (8u << ch)) {
-      v = kInf;
+    } else if (pinf || ninf) {
+      v = pinf ? kInf : -kInf;
     } else {
-      long long sum = (long long)P.accum[(size_t)ch * P.npix + lp];
-      v = (float)((double)sum * 2.3283064365386963e-10 * scale);
+      const size_t i = (size_t)ch * P.npix + lp;
+      const long long sum = (long long)P.accum[i];
+      v = (float)(((double)sum * 2.3283064365386963e-10 + P.side[i]) * scale);
     }
     out[3 * (size_t)lp + ch] = v;
   }
@@ -317,11 +343,12 @@ struct RenderState {
   hipStream_t own_stream = nullptr;
   std::vector<void*> allocs;
   F4 *ray_o = nullptr, *ray_d = nullptr, *hit = nullptr, *pend = nullptr, *pre = nullptr,
-     *acc = nullptr, *stack = nullptr;
+     *stack = nullptr;
   uint2* path = nullptr;
   uint32_t* queue[2] = {nullptr, nullptr};
   Counters* ctr = nullptr;
   unsigned long long* accum = nullptr;
+  double* side = nullptr;
   uint32_t* pflags = nullptr;
   uint32_t* ostack = nullptr;
   uint32_t ostack_cols = 0;
@@ -343,10 +370,25 @@ struct RenderState {
 };
 
 void release_device(Scene* s) {
-  delete s->dev;
-  s->dev = nullptr;
-  delete s->state;
-  s->state = nullptr;
+  std::lock_guard<std::mutex> lk(s->mu);
+  for (auto& kv : s->slots) {
+    if (kv.second->st) {
+      (void)hipSetDevice(kv.first.first);
+      delete kv.second->st;
+    }
+    delete kv.second;
+  }
+  s->slots.clear();
+  for (auto& kv : s->devs) {
+    (void)hipSetDevice(kv.first);
+    delete kv.second;
+  }
+  s->devs.clear();
+  if (s->multi_buf) {
+    (void)hipSetDevice(s->multi_dev);
+    (void)hipFree(s->multi_buf);
+    s->multi_buf = nullptr;
+  }
 }
 
 template <typename T>
@@ -427,13 +469,30 @@ static void make_record(const HostScene& h, uint32_t ref, F4* r) {
   }
 }
 
-static int ensure_scene(Scene* s, int device) {
-  if (s->dev && s->dev->device == device) return RT_OK;
-  delete s->dev;
-  s->dev = new DeviceScene();
-  s->dev->device = device;
+// the scene's device copy on `device` (uploaded on first use, then shared by every
+// slot on that device; read-only while rendering)
+static int upload_scene(const Scene* s, DeviceScene* ds);
+static int ensure_scene(Scene* s, int device, DeviceScene** out) {
+  std::lock_guard<std::mutex> lk(s->mu);
+  auto it = s->devs.find(device);
+  if (it != s->devs.end()) {
+    *out = it->second;
+    return RT_OK;
+  }
+  DeviceScene* ds = new DeviceScene();
+  ds->device = device;
+  const int rc = upload_scene(s, ds);
+  if (rc != RT_OK) {
+    delete ds;
+    return rc;
+  }
+  s->devs[device] = ds;
+  *out = ds;
+  return RT_OK;
+}
+static int upload_scene(const Scene* s, DeviceScene* ds) {
   const HostScene& h = s->h;
-  DevScene& d = s->dev->d;
+  DevScene& d = ds->d;
   // per-material "texture reads u,v" flag for sphere UV (stored in the pad)
   std::vector<DevMaterial> mats = h.mats;
   for (auto& m : mats) {
@@ -455,7 +514,7 @@ static int ensure_scene(Scene* s, int device) {
   }
   int rc;
 #define UP(vec, field)                                      \
-  if ((rc = upload(s->dev, vec, &d.field)) != RT_OK) return rc;
+  if ((rc = upload(ds, vec, &d.field)) != RT_OK) return rc;
   UP(h.sph_cr, sph_cr);
   UP(h.sph_mv, sph_mv);
   UP(h.sph_uv, sph_uv);
@@ -463,9 +522,9 @@ static int ensure_scene(Scene* s, int device) {
   UP(h.tri, tri);
   UP(h.tri_attr, tri_attr);
   UP(h.nodes4, nodes);
-  if ((rc = upload(s->dev, h.nodes, &s->dev->nodes2)) != RT_OK) return rc;
-  s->dev->root2 = h.root;
-  s->dev->n_nodes2 = (int32_t)(h.nodes.size() / 4);
+  if ((rc = upload(ds, h.nodes, &ds->nodes2)) != RT_OK) return rc;
+  ds->root2 = h.root;
+  ds->n_nodes2 = (int32_t)(h.nodes.size() / 4);
   UP(h.refs, refs);
   {
     std::vector<F4> recs, lrecs;
@@ -543,8 +602,8 @@ static int ensure_scene(Scene* s, int device) {
                            r[2].y, r[2].z, r[3].x, r[3].y, r[3].z, kb,     r[0].w};
       for (int e = 0; e < 15; ++e) f[2 * e] = v[e];
     }
-    s->dev->brute_slots = slots.size();
-    if ((rc = upload(s->dev, pairs, &s->dev->brute_pairs)) != RT_OK) return rc;
+    ds->brute_slots = slots.size();
+    if ((rc = upload(ds, pairs, &ds->brute_pairs)) != RT_OK) return rc;
   }
   UP(h.media, media);
   UP(h.medium_refs, medium_refs);
@@ -575,28 +634,30 @@ static int dalloc(RenderState* st, T** p, size_t count) {
 
 // slot-indexed wavefront buffers (only for WAVEFRONT) + the weight stack,
 // counters and pixel accumulators (both modes)
-static int ensure_state(Scene* s, int device, uint32_t P, int depth_cap, uint32_t npix, bool soa) {
-  RenderState* st = s->state;
+static int ensure_state(SlotState* slot, int device, uint32_t P, int depth_cap, uint32_t npix,
+                        bool soa) {
+  RenderState* st = slot->st;
   if (st && (st->device != device || st->P < P || st->depth_cap < depth_cap || st->npix < npix ||
              (soa && !st->ray_o))) {
     delete st;
-    st = s->state = nullptr;
+    st = slot->st = nullptr;
   }
   if (st) return RT_OK;
-  st = s->state = new RenderState();
+  st = slot->st = new RenderState();
   st->device = device;
   st->P = P;
   st->depth_cap = depth_cap;
   st->npix = npix;
   int rc;
   if ((rc = dalloc(st, &st->stack, (size_t)P * depth_cap)) || (rc = dalloc(st, &st->ctr, 1)) ||
-      (rc = dalloc(st, &st->accum, 3 * (size_t)npix)) || (rc = dalloc(st, &st->pflags, npix)) ||
+      (rc = dalloc(st, &st->accum, 3 * (size_t)npix)) || (rc = dalloc(st, &st->side, 3 * (size_t)npix)) ||
+      (rc = dalloc(st, &st->pflags, npix)) ||
       (rc = dalloc(st, &st->out, 3 * (size_t)npix)))
     return rc;
   if (soa &&
       ((rc = dalloc(st, &st->ray_o, P)) || (rc = dalloc(st, &st->ray_d, P)) ||
        (rc = dalloc(st, &st->hit, P)) || (rc = dalloc(st, &st->pend, P)) ||
-       (rc = dalloc(st, &st->pre, P)) || (rc = dalloc(st, &st->acc, P)) ||
+       (rc = dalloc(st, &st->pre, P)) ||
        (rc = dalloc(st, &st->path, P)) || (rc = dalloc(st, &st->queue[0], (size_t)kXcd * P)) ||
        (rc = dalloc(st, &st->queue[1], (size_t)kXcd * P))))
     return rc;
@@ -651,8 +712,17 @@ static const void* pick_fused(bool lds, uint32_t set, int tree) {
   return lds ? fused_for<true>(set) : fused_for<false>(set);
 }
 
+// rt_render_multi's share hand-off: after the resolve, the share's image (rows of
+// this rank, [rows][W][3]) is copied to `dst` on device `dst_device` (peer copy over
+// xGMI when the devices differ) on the share's stream, before the render returns.
+struct Gather {
+  float* dst;
+  int dst_device;
+};
+
 static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_opts* opts,
-                       float* out_host, float* out_dev, rt_stats* stats) {
+                       float* out_host, float* out_dev, rt_stats* stats, int slot_id = 0,
+                       const Gather* gather = nullptr) {
   if (!scene || !cam) return set_error(RT_ERR_INVALID, "rt_render: null scene/camera");
   rt_render_opts o{};
   if (opts) o = *opts;
@@ -670,7 +740,17 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     return set_error(RT_ERR_INVALID, "rt_render: device %d of %d", o.device, ndev);
   HIP_OK(hipSetDevice(o.device));
   Scene* s = &scene->s;
-  if ((rc = ensure_scene(s, o.device))) return rc;
+  DeviceScene* ds = nullptr;
+  if ((rc = ensure_scene(s, o.device, &ds))) return rc;
+  SlotState* slot = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(s->mu);
+    SlotState*& sl = s->slots[{o.device, slot_id}];
+    if (!sl) sl = new SlotState();
+    slot = sl;
+  }
+  std::lock_guard<std::mutex> inflight(slot->mu);  // one render per (scene, device, slot)
+  const bool track = slot_id == 0;  // rt_progress follows rt_render; rt_render_multi sets its own
 
   const uint32_t W = (uint32_t)cd.width, H = (uint32_t)cd.height;
   const uint32_t rows = H > (uint32_t)o.rank ? (H - (uint32_t)o.rank + o.nranks - 1) / o.nranks : 0;
@@ -716,7 +796,7 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
       (env_tree == 4 || (!s->h.nodes.empty() && s->h.nodes.size() / 4 + n_refs <= slots_for(2))))
     tree = env_tree;  // A/B override
   const size_t lds_slots = slots_for(tree);
-  const size_t brute_slots = s->dev->brute_slots;  // record-loop pairs, 2 x 64 B each
+  const size_t brute_slots = ds->brute_slots;  // record-loop pairs, 2 x 64 B each
   const int smem_env = env_int("RT_BRUTE_SMEM", -1);
   const bool brute_smem =
       tree == 0 && (smem_env >= 0 ? smem_env != 0 : brute_slots > lds_slots);
@@ -761,10 +841,10 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     P = std::max<uint32_t>(256u, std::min<uint32_t>(P, std::max<uint32_t>(n_chunks, 256u)));
     P = (P + 255u) & ~255u;
   }
-  if ((rc = ensure_state(s, o.device, P, depth_cap, std::max<uint32_t>(npix, 1),
+  if ((rc = ensure_state(slot, o.device, P, depth_cap, std::max<uint32_t>(npix, 1),
                          mode == RT_MODE_WAVEFRONT)))
     return rc;
-  RenderState* st = s->state;
+  RenderState* st = slot->st;
   const void* extend_kernel =
       lds_nodes ? (const void*)k_extend<true> : (const void*)k_extend<false>;
   if (mode == RT_MODE_WAVEFRONT && st->resident_blocks == 0 &&
@@ -791,14 +871,14 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   }
 
   Params p{};
-  p.sc = s->dev->d;
+  p.sc = ds->d;
   if (tree == 2) {
-    p.sc.nodes = s->dev->nodes2;
-    p.sc.root = s->dev->root2;
-    p.sc.n_nodes = s->dev->n_nodes2;
+    p.sc.nodes = ds->nodes2;
+    p.sc.root = ds->root2;
+    p.sc.n_nodes = ds->n_nodes2;
   } else if (tree == 0) {
     p.sc.n_nodes = 0;  // records only (stage_nodes puts them at the start of the cache)
-    p.sc.leafprims = s->dev->brute_pairs;
+    p.sc.leafprims = ds->brute_pairs;
     p.sc.n_refs = (int32_t)brute_slots;  // even: whole pairs
   }
   for (int i = 0; i < 3; ++i) {
@@ -846,12 +926,15 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   p.path = st->path;
   p.pend = st->pend;
   p.pre = st->pre;
-  p.acc = st->acc;
+
   p.stack = st->stack;
   p.queue[0] = st->queue[0];
   p.queue[1] = st->queue[1];
   p.ctr = st->ctr;
   p.accum = st->accum;
+  p.side = st->side;
+  // |v| < 2^31 / ss: the ss-sample fixed-point sum of a pixel stays inside int64
+  p.vlim = std::nextafter((float)(2147483648.0 / (double)std::max<uint32_t>(ss, 1u)), 0.0f);
   p.pflags = st->pflags;
   p.ostack = st->ostack;
   p.stack_cols = st->ostack_cols;
@@ -883,6 +966,7 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   HIP_OK(hipMemsetAsync(st->ctr, 0, sizeof(Counters), stream));
   if (npix > 0) {
     HIP_OK(hipMemsetAsync(st->accum, 0, 3 * (size_t)npix * sizeof(unsigned long long), stream));
+    HIP_OK(hipMemsetAsync(st->side, 0, 3 * (size_t)npix * sizeof(double), stream));
     HIP_OK(hipMemsetAsync(st->pflags, 0, (size_t)npix * sizeof(uint32_t), stream));
   }
   int iterations = 0;
@@ -897,7 +981,7 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     st->prog_events.push_back(e);
   }
-  {
+  if (track) {
     std::lock_guard<std::mutex> lk(s->prog.mu);
     s->prog.total = (uint64_t)npix * ss;
     s->prog.done = 0;
@@ -915,13 +999,15 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   }
   struct ProgressDone {  // every return path below ends the in-flight state
     Progress& p;
+    bool track;
     bool ok = false;
     ~ProgressDone() {
+      if (!track) return;
       std::lock_guard<std::mutex> lk(p.mu);
       if (ok) p.done = p.total;
       p.busy = 0;
     }
-  } prog_done{s->prog};
+  } prog_done{s->prog, track};
   if (n_chunks > 0 && mode == RT_MODE_FUSED) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (prof) {
@@ -1014,6 +1100,9 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   if (out_host && npix > 0)
     HIP_OK(hipMemcpyAsync(out_host, dst, 3 * (size_t)npix * sizeof(float), hipMemcpyDeviceToHost,
                           stream));
+  if (gather && npix > 0)
+    HIP_OK(hipMemcpyPeerAsync(gather->dst, gather->dst_device, dst, o.device,
+                              3 * (size_t)npix * sizeof(float), stream));
   HIP_OK(hipStreamSynchronize(stream));
   prog_done.ok = true;
   auto t_end = std::chrono::steady_clock::now();
@@ -1029,6 +1118,7 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     stats->samples = (uint64_t)npix * ss;
     stats->segments = hc.segments;
     stats->stack_pushes = hc.pushes;
+    stats->overflow_samples = hc.overflow;
     stats->extend_rays = hc.segments;
     stats->shade_rays = hc.segments;
     stats->ms_total = std::chrono::duration<double, std::milli>(t_end - t_start).count();
@@ -1060,9 +1150,158 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   return RT_OK;
 }
 
+// rows of share i ([rows_per][W][3] at gather + i*rows_per*W*3) -> image rows r = i + n*k
+__global__ __launch_bounds__(256) void k_deinterleave(const float* gather, float* out, uint32_t H,
+                                                      uint32_t W, uint32_t n, uint32_t rows_per) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t row_floats = 3ull * W;
+  if (i >= (uint64_t)H * row_floats) return;
+  const uint32_t r = (uint32_t)(i / row_floats);
+  const uint64_t x = i - (uint64_t)r * row_floats;
+  out[i] = gather[((uint64_t)(r % n) * rows_per + r / n) * row_floats + x];
+}
+
+// rt_render_multi: share i (rows r % n == i, camera.go:119-122) on devices[i], one
+// host thread and stream per share, each with its own render slot; the shares are
+// peer-copied to devices[0] and de-interleaved there.
+static int render_multi(rt_scene* scene, const rt_camera* cam, const rt_render_opts* opts,
+                        const int32_t* devices, int32_t n, float* out_host, float* out_dev,
+                        rt_stats* stats) {
+  if (!scene || !cam || !devices || n <= 0)
+    return set_error(RT_ERR_INVALID, "rt_render_multi: null argument or n <= 0");
+  rt_render_opts o{};
+  if (opts) o = *opts;
+  if (o.nranks > 1 || o.rank != 0)
+    return set_error(RT_ERR_INVALID, "rt_render_multi: shards the image itself (rank/nranks)");
+  if (o.stream) return set_error(RT_ERR_INVALID, "rt_render_multi: one stream per share (opts.stream)");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return set_error(RT_ERR_DEVICE, "rt_render_multi: no HIP device available");
+  for (int i = 0; i < n; ++i)
+    if (devices[i] < 0 || devices[i] >= ndev)
+      return set_error(RT_ERR_INVALID, "rt_render_multi: device %d of %d", devices[i], ndev);
+  rt_camera_derived cd;
+  int rc = rt_camera_derive(cam, &cd);
+  if (rc) return rc;
+  Scene* s = &scene->s;
+  std::lock_guard<std::mutex> multi(s->multi_mu);
+  const auto t0 = std::chrono::steady_clock::now();
+  const uint32_t H = (uint32_t)cd.height, W = (uint32_t)cd.width, N = (uint32_t)n;
+  const uint32_t rows_per = (H + N - 1) / N;
+  const size_t gather_floats = (size_t)N * rows_per * W * 3, img_floats = (size_t)H * W * 3;
+  const int d0 = devices[0];
+  HIP_OK(hipSetDevice(d0));
+  const size_t need = (gather_floats + img_floats) * sizeof(float);
+  if (!s->multi_buf || s->multi_dev != d0 || s->multi_bytes < need) {
+    if (s->multi_buf) {
+      (void)hipSetDevice(s->multi_dev);
+      (void)hipFree(s->multi_buf);
+      s->multi_buf = nullptr;
+      HIP_OK(hipSetDevice(d0));
+    }
+    HIP_OK(hipMalloc(&s->multi_buf, std::max<size_t>(need, 4)));
+    s->multi_bytes = need;
+    s->multi_dev = d0;
+  }
+  float* gbuf = (float*)s->multi_buf;
+  float* img = out_dev ? out_dev : gbuf + gather_floats;
+  for (int i = 1; i < n; ++i)  // xGMI peer access both ways (already enabled is fine)
+    if (devices[i] != d0) {
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, devices[i], d0) == hipSuccess && can) {
+        HIP_OK(hipSetDevice(devices[i]));
+        (void)hipDeviceEnablePeerAccess(d0, 0);
+        HIP_OK(hipSetDevice(d0));
+        (void)hipDeviceEnablePeerAccess(devices[i], 0);
+      }
+      (void)hipGetLastError();
+    }
+  {
+    std::lock_guard<std::mutex> lk(s->prog.mu);
+    s->prog.total = (uint64_t)H * W * cd.spp_sqrt * cd.spp_sqrt;
+    s->prog.done = 0;
+    s->prog.events.clear();
+    s->prog.cum.clear();
+    s->prog.busy = 1;
+  }
+  std::vector<rt_stats> st(n);
+  std::vector<int> rcs(n, RT_OK);
+  std::vector<std::string> errs(n);
+  std::vector<std::thread> th;
+  for (int i = 0; i < n; ++i)
+    th.emplace_back([&, i] {
+      rt_render_opts oi = o;
+      oi.device = devices[i];
+      oi.rank = i;
+      oi.nranks = n;
+      oi.progress_slices = 0;
+      const Gather g = {gbuf + (size_t)i * rows_per * W * 3, d0};
+      rcs[i] = render_impl(scene, cam, &oi, nullptr, nullptr, &st[i], 1 + i, &g);
+      if (rcs[i] != RT_OK) errs[i] = rt_last_error();
+    });
+  for (auto& t : th) t.join();
+  {
+    std::lock_guard<std::mutex> lk(s->prog.mu);
+    s->prog.busy = 0;
+  }
+  for (int i = 0; i < n; ++i)
+    if (rcs[i] != RT_OK) return set_error(rcs[i], "rt_render_multi share %d: %s", i, errs[i].c_str());
+  HIP_OK(hipSetDevice(d0));
+  if (img_floats > 0) {
+    hipLaunchKernelGGL(k_deinterleave, dim3((unsigned)((img_floats + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)0, gbuf, img, H, W, N, rows_per);
+    HIP_OK(hipGetLastError());
+    if (out_host)
+      HIP_OK(hipMemcpy(out_host, img, img_floats * sizeof(float), hipMemcpyDeviceToHost));
+  }
+  HIP_OK(hipDeviceSynchronize());
+  {
+    std::lock_guard<std::mutex> lk(s->prog.mu);
+    s->prog.done = s->prog.total;
+  }
+  if (stats) {
+    memset(stats, 0, sizeof *stats);
+    *stats = st[0];
+    stats->samples = stats->segments = stats->stack_pushes = stats->overflow_samples = 0;
+    stats->extend_rays = stats->shade_rays = 0;
+    stats->rows = 0;
+    stats->ms_fused = stats->ms_extend = stats->ms_shade = 0;
+    for (int i = 0; i < n; ++i) {
+      stats->samples += st[i].samples;
+      stats->segments += st[i].segments;
+      stats->stack_pushes += st[i].stack_pushes;
+      stats->overflow_samples += st[i].overflow_samples;
+      stats->extend_rays += st[i].extend_rays;
+      stats->shade_rays += st[i].shade_rays;
+      stats->rows += st[i].rows;
+      // the slowest share bounds the render
+      stats->ms_fused = std::max(stats->ms_fused, st[i].ms_fused);
+      stats->ms_extend = std::max(stats->ms_extend, st[i].ms_extend);
+      stats->ms_shade = std::max(stats->ms_shade, st[i].ms_shade);
+    }
+    stats->ms_total =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return RT_OK;
+}
+
 }  // namespace rt
 
 extern "C" {
+
+int rt_render_multi(rt_scene* s, const rt_camera* cam, const rt_render_opts* opts,
+                    const int32_t* devices, int32_t n, float* out_rgb, rt_stats* stats) {
+  if (!out_rgb) return rt::set_error(RT_ERR_INVALID, "rt_render_multi: null output");
+  return rt::render_multi(s, cam, opts, devices, n, out_rgb, nullptr, stats);
+}
+
+int rt_render_multi_device(rt_scene* s, const rt_camera* cam, const rt_render_opts* opts,
+                           const int32_t* devices, int32_t n, float* out_rgb_device,
+                           rt_stats* stats) {
+  if (!out_rgb_device) return rt::set_error(RT_ERR_INVALID, "rt_render_multi_device: null output");
+  return rt::render_multi(s, cam, opts, devices, n, nullptr, out_rgb_device, stats);
+}
+
 
 int rt_render(rt_scene* s, const rt_camera* cam, const rt_render_opts* opts, float* out_rgb,
               rt_stats* stats) {

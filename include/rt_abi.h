@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 enum {
   RT_OK = 0,
@@ -352,16 +352,41 @@ typedef struct {
   int32_t lds_scene;       /* 1: nodes (and leaf records) ran from the LDS cache */
   int32_t chunk_samples;   /* samples per work chunk (opts.chunk or the adaptive choice) */
   int32_t _pad2;
+  /* sample channels with |v| >= 2^31 / spp_sqrt^2 (outside the exact fixed-point pixel
+   * sum; added in fp64 instead — the image is then order-dependent in those pixels) */
+  uint64_t overflow_samples;
 } rt_stats;
 
 /* Render this rank's rows; out_rgb (host) receives linear mean RGB
- * [rows][W][3] fp32, rows = rows r with r % nranks == rank in increasing order. */
+ * [rows][W][3] fp32, rows = rows r with r % nranks == rank in increasing order.
+ * Replaces (*Camera).Render's pixel loop, camera.go:156 -> :90-153 (one process,
+ * one device; rank/nranks = the row partition of camera.go:119-122 across processes).
+ * Threading: an rt_scene keeps one device copy per device ordinal and one set of
+ * render buffers per device; rt_render / rt_render_device may run concurrently from
+ * different threads for DIFFERENT devices of one scene; calls for the same device
+ * serialise (the second waits for the first). */
 int rt_render(rt_scene* s, const rt_camera* cam, const rt_render_opts* opts, float* out_rgb,
               rt_stats* stats);
 /* Same, but out_rgb is a device pointer on opts->device (e.g. a torch tensor);
  * work is enqueued on opts->stream and the call returns after it completes. */
 int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_render_opts* opts,
                      float* out_rgb_device, rt_stats* stats);
+
+/* Render the WHOLE image on n devices from one process (the north_star's 8-GPU tile
+ * split, camera.go:119-122 row partition): device devices[i] renders rows
+ * r % n == i, each share on its own host thread, stream and render buffers (a
+ * device may repeat: {0, 0, 0} renders three shares on device 0); the shares are
+ * copied to devices[0] (peer copies over xGMI) and de-interleaved there by a kernel.
+ * out_rgb (host) receives [H][W][3]; the _device form writes a device pointer on
+ * devices[0].  The image is bit-identical to rt_render's for any n (per-sample
+ * fixed-point pixel sums).  opts->rank/nranks must be 0/1 and opts->stream NULL;
+ * stats sum samples/segments over shares, ms_fused is the slowest share's.
+ * One rt_render_multi per scene at a time (a second call waits). */
+int rt_render_multi(rt_scene* s, const rt_camera* cam, const rt_render_opts* opts,
+                    const int32_t* devices, int32_t n, float* out_rgb, rt_stats* stats);
+int rt_render_multi_device(rt_scene* s, const rt_camera* cam, const rt_render_opts* opts,
+                           const int32_t* devices, int32_t n, float* out_rgb_device,
+                           rt_stats* stats);
 
 /* Progress of the render in flight on scene s (the reference's progress bar,
  * camera.go:106-108 + internal/progress): may be polled from any thread while

@@ -1,4 +1,10 @@
-"""Parity metrics between the HIP path and the CPU oracle (shared by tests)."""
+"""Parity metrics between the HIP path and the CPU oracle (shared by tests).
+
+Set PARITY_LOG=path to append every comparison (test id + metrics) as a JSON line:
+that is how the thresholds in the tests were calibrated (DESIGN.md "Parity")."""
+import json
+import os
+
 import numpy as np
 
 
@@ -8,12 +14,15 @@ def compare(gpu_img, ref_img):
     g = np.asarray(gpu_img, np.float64)
     r = np.asarray(ref_img, np.float64)
     fin = np.isfinite(g) & np.isfinite(r)
-    diff = np.where(fin, np.abs(g - r), np.where(np.isnan(g) == np.isnan(r), 0.0, np.inf))
-    tol = 1e-3 * np.maximum(1.0, np.nan_to_num(np.abs(r), nan=1.0, posinf=1.0))
+    # non-finite pairs agree only when identical (both NaN, or the same infinity)
+    same = (np.isnan(g) & np.isnan(r)) | (g == r)
+    diff = np.where(fin, np.abs(g - r), np.where(same, 0.0, np.inf))
+    # |delta| <= 2^-10 * max(1, |ref|)
+    tol = 2.0 ** -10 * np.maximum(1.0, np.nan_to_num(np.abs(r), nan=1.0, posinf=1.0))
     q_g = rt.quantize(gpu_img).astype(np.int32)
     q_r = rt.quantize(ref_img).astype(np.int32)
     dq = np.abs(q_g - q_r)
-    return {
+    m = {
         "frac_close": float(np.mean(diff <= tol)),
         "max_abs": float(np.max(np.where(np.isfinite(diff), diff, 0))),
         "mean_abs": float(np.mean(np.where(np.isfinite(diff), diff, 0))),
@@ -22,3 +31,8 @@ def compare(gpu_img, ref_img):
         "mean_gpu": g[np.isfinite(g)].mean() if np.isfinite(g).any() else float("nan"),
         "mean_ref": r[np.isfinite(r)].mean() if np.isfinite(r).any() else float("nan"),
     }
+    if os.environ.get("PARITY_LOG"):
+        with open(os.environ["PARITY_LOG"], "a") as f:
+            f.write(json.dumps({"test": os.environ.get("PYTEST_CURRENT_TEST", ""),
+                                **{k: float(v) for k, v in m.items()}}) + "\n")
+    return m

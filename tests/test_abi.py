@@ -33,7 +33,7 @@ def test_bindings_cover_header(rt):
 
 
 def test_abi_version(rt):
-    assert rt.lib().rt_abi_version() == 1
+    assert rt.lib().rt_abi_version() == 2  # 2: rt_render_multi, rt_stats.overflow_samples
 
 
 @pytest.mark.skipif(shutil.which("gcc") is None, reason="no C compiler")
@@ -76,3 +76,12 @@ def test_progress_without_render(rt):
     t, cam, w, l = rt.demo_scene("cornell")
     with rt.Scene(t, w, l) as sc:
         assert sc.progress() == (0, 0)
+
+
+def test_render_multi_argument_errors(rt):
+    """rt_render_multi validates its arguments before touching a device."""
+    t, cam, w, l = rt.demo_scene("cornell")
+    cam.Width, cam.SamplesPerPixel = 8, 1
+    with rt.Scene(t, w, l) as sc:
+        with pytest.raises(rt.RtError):
+            sc.render_multi(cam, [])

@@ -47,11 +47,11 @@ def test_ragged_row_shards_are_bitwise(rt, gpu):
     cam.Width, cam.SamplesPerPixel, cam.AspectRatio = 37, 9, 1.3  # H = 28
     H = cam.derived().height
     with rt.Scene(t, w, l) as sc:
-        full, _ = sc.render(cam, seed=2, chunk=8)
+        full, _ = sc.render(cam, seed=2)
         for n in (3, 5, 29, 40):  # more ranks than rows: some shards are empty
             rows = 0
             for r in range(n):
-                part, st = sc.render(cam, seed=2, rank=r, nranks=n, chunk=8)
+                part, st = sc.render(cam, seed=2, rank=r, nranks=n)
                 assert np.array_equal(part, full[r::n]), (n, r)
                 rows += part.shape[0]
             assert rows == H

@@ -1,7 +1,9 @@
 """Per-feature GPU-vs-oracle parity: one small scene per reference feature.
 
-Tolerance as in test_parity_gpu.py: >= 99 % of linear-RGB
-channels within 1e-3 * max(1, |ref|), 8-bit output equal for >= 99 %.
+Tolerance: >= 99.5 % of linear-RGB channels within
+2^-10 * max(1, |ref|); 8-bit output equal for >= 99 % (calibrated: these 32x32-ish
+images at 9-25 spp put ~3 k channels per test, so one forked sample in a bright
+pixel is 0.03 %; measured worst 99.41 %, `cluster` on the wavefront kernels).
 """
 import os
 
@@ -25,5 +27,5 @@ def test_feature_parity(rt, oracle, gpu, name, mode):
     print(name, mode, m, st["segments"], ost["segments"])
     assert st["samples"] == ost["samples"]
     assert abs(st["segments"] - ost["segments"]) <= 0.01 * ost["segments"] + 10
-    assert m["frac_close"] >= 0.99, m
+    assert m["frac_close"] >= 0.995, m
     assert m["q_equal"] >= 0.99, m

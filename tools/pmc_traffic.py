@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
-"""Collect PMC counters for bench.py's kernels with rocprofv3, one --pmc pass per
-counter group (MI355X_MICROARCH.md "HBM" / "rocprofv3 PMC slots"), and write
-per-launch HBM traffic + SQ activity to a JSON file.
+"""PMC counters of the fused kernel per BASELINE config with rocprofv3, one --pmc
+pass per counter group (MI355X_MICROARCH.md "HBM" / "rocprofv3 PMC slots"), merged
+into a copy of profiles/traffic.json (read by bench.py's roofline) plus the raw
+per-config counters <tag>_pmc_<config>.json, all written to gpurun_out/profiles_<tag>/
+(the box returns only gpurun_out/; copy the files into profiles/ afterwards).
 
   FETCH_SIZE / WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE reads exactly half
   the bytes of a wide coalesced streaming read (the guide's correction: double
@@ -10,7 +12,7 @@ per-launch HBM traffic + SQ activity to a JSON file.
   (kernel-trace only), never combined with sys/runtime tracing.
 
 usage (on the GPU box, from the repo root):
-  python3 tools/pmc_traffic.py OUT.json [bench args ...]
+  python3 tools/pmc_traffic.py TAG C2 C3 C4 C5
 """
 import csv
 import glob
@@ -19,6 +21,9 @@ import os
 import subprocess
 import sys
 
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CONFIGS = {"C2": ("cornell", 800, 1024), "C3": ("book1", 1200, 512),
+           "C4": ("book2", 800, 4096), "C5": ("model", 1920, 1024)}
 PASSES = [
     ["FETCH_SIZE"],
     ["WRITE_SIZE"],
@@ -30,26 +35,24 @@ PASSES = [
 ]
 
 
-def run_pass(repo, tag, counters, bench_args):
-    outdir = os.path.join(repo, "gpurun_out", f"pmc_{tag}")
+def run_pass(tag, counters, bench_args):
+    outdir = os.path.join(REPO, "gpurun_out", f"pmc_{tag}")
     cmd = ["rocprofv3", "--kernel-trace", "--pmc", *counters, "-f", "csv", "-d", outdir, "-o", "run",
-           "--", sys.executable, os.path.join(repo, "bench.py"), "--no-cpu-baseline", *bench_args]
+           "--", sys.executable, os.path.join(REPO, "bench.py"), "--no-cpu-baseline",
+           "--no-extra-configs", *bench_args]
     env = dict(os.environ, TMPDIR="/tmp")
-    r = subprocess.run(["timeout", "-k", "10", "600", *cmd], cwd="/tmp", env=env,
+    r = subprocess.run(["timeout", "-k", "10", "300", *cmd], cwd="/tmp", env=env,
                        stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     if r.returncode != 0:
         raise SystemExit(f"rocprofv3 pass {counters} failed ({r.returncode}):\n{r.stdout[-3000:]}")
-    files = glob.glob(os.path.join(outdir, "**", "*counter_collection*.csv"), recursive=True)
-    vals = {}  # kernel -> counter -> [per dispatch]
-    for fn in files:
+    vals = {}  # kernel -> counter -> dispatch -> value
+    for fn in glob.glob(os.path.join(outdir, "**", "*counter_collection*.csv"), recursive=True):
         with open(fn) as f:
             for row in csv.DictReader(f):
-                k = row.get("Kernel_Name", "")
-                c = row.get("Counter_Name", "")
-                v = float(row.get("Counter_Value", "nan"))
+                k, c = row.get("Kernel_Name", ""), row.get("Counter_Name", "")
                 d = row.get("Dispatch_Id", "0")
                 vals.setdefault(k, {}).setdefault(c, {}).setdefault(d, 0.0)
-                vals[k][c][d] += v
+                vals[k][c][d] += float(row.get("Counter_Value", "nan"))
     return vals
 
 
@@ -60,43 +63,75 @@ def short(name):
     return None
 
 
-def main():
-    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    out = sys.argv[1]
-    bench_args = sys.argv[2:] or ["--steps", "1", "--warmup", "1"]
+def collect(tag, cfg):
+    scene, width, spp = CONFIGS[cfg]
+    bench_args = ["--scene", scene, "--width", str(width), "--spp", str(spp),
+                  "--steps", "1", "--warmup", "1"]
     merged = {}
     for i, counters in enumerate(PASSES):
-        vals = run_pass(repo, f"p{i}", counters, bench_args)
-        for k, cs in vals.items():
+        for k, cs in run_pass(f"{tag}_{cfg}_p{i}", counters, bench_args).items():
             s = short(k)
             if not s:
                 continue
             for c, per_disp in cs.items():
                 xs = list(per_disp.values())
-                merged.setdefault(s, {})[c] = {"per_launch_mean": sum(xs) / len(xs), "launches": len(xs)}
+                merged.setdefault(s, {})[c] = {"per_launch_mean": sum(xs) / len(xs),
+                                               "launches": len(xs)}
     res = {}
     for k, cs in merged.items():
         g = {c: v["per_launch_mean"] for c, v in cs.items()}
-        fetch_kb = g.get("FETCH_SIZE")
-        write_kb = g.get("WRITE_SIZE")
-        entry = {"counters_per_launch": g,
-                 "launches": max(v["launches"] for v in cs.values())}
-        if fetch_kb is not None and write_kb is not None:
-            entry["fetch_bytes_raw"] = fetch_kb * 1024
-            entry["write_bytes"] = write_kb * 1024
+        e = {"counters_per_launch": g, "launches": max(v["launches"] for v in cs.values())}
+        if "FETCH_SIZE" in g and "WRITE_SIZE" in g:
+            e["fetch_bytes_raw"] = g["FETCH_SIZE"] * 1024
+            e["write_bytes"] = g["WRITE_SIZE"] * 1024
             # gfx950 correction from MI355X_MICROARCH.md (exact for wide streaming reads)
-            entry["hbm_bytes_per_launch"] = (2 * fetch_kb + write_kb) * 1024
-            entry["hbm_bytes_per_launch_uncorrected"] = (fetch_kb + write_kb) * 1024
-        if "SQ_INSTS_VALU" in g and "SQ_WAVES" in g:
-            entry["valu_insts_per_wave"] = g["SQ_INSTS_VALU"] / max(g["SQ_WAVES"], 1)
-        if "SQ_ACTIVE_INST_VALU" in g and "SQ_WAVE_CYCLES" in g:
-            entry["valu_active_frac_of_wave_cycles"] = g["SQ_ACTIVE_INST_VALU"] / max(g["SQ_WAVE_CYCLES"], 1)
+            e["hbm_bytes_per_launch"] = (2 * g["FETCH_SIZE"] + g["WRITE_SIZE"]) * 1024
+            e["hbm_bytes_per_launch_uncorrected"] = (g["FETCH_SIZE"] + g["WRITE_SIZE"]) * 1024
+        if "SQ_INSTS_VALU" in g:
+            e["valu_insts_per_launch"] = g["SQ_INSTS_VALU"]
+            e["salu_insts_per_launch"] = g.get("SQ_INSTS_SALU")
         if "SQ_WAIT_ANY" in g and "SQ_WAVE_CYCLES" in g:
-            entry["wait_frac_of_wave_cycles"] = g["SQ_WAIT_ANY"] / max(g["SQ_WAVE_CYCLES"], 1)
-        res[k] = entry
-    with open(out, "w") as f:
-        json.dump({"bench_args": bench_args, "kernels": res}, f, indent=1)
-    print(json.dumps(res, indent=1)[:4000])
+            e["wait_frac_of_wave_cycles"] = g["SQ_WAIT_ANY"] / max(g["SQ_WAVE_CYCLES"], 1)
+        if "SQ_ACTIVE_INST_VALU" in g and "SQ_WAVE_CYCLES" in g:
+            e["valu_active_frac_of_wave_cycles"] = g["SQ_ACTIVE_INST_VALU"] / max(g["SQ_WAVE_CYCLES"], 1)
+        res[k] = e
+    return scene, bench_args, res
+
+
+def main():
+    sys.path.insert(0, REPO)
+    import go_raytracer_amd as rt
+    tag, cfgs = sys.argv[1], sys.argv[2:] or list(CONFIGS)
+    try:
+        with open(os.path.join(REPO, "profiles", "traffic.json")) as f:
+            db = json.load(f)
+    except (OSError, ValueError):
+        db = {}
+    out_dir = os.path.join(REPO, "gpurun_out", f"profiles_{tag}")
+    os.makedirs(out_dir, exist_ok=True)
+    tpath = os.path.join(out_dir, "traffic.json")
+    db["_source"] = ("tools/pmc_traffic.py: 5 separate --pmc passes per config, kernel-trace "
+                     "only; FETCH_SIZE doubled (MI355X_MICROARCH.md gfx950 correction); raw "
+                     "counters in profiles/<tag>_pmc_<config>.json")
+    for cfg in cfgs:
+        scene, bench_args, res = collect(tag, cfg)
+        _, cam, _, _ = rt.demo_scene(scene)
+        cam.Width, cam.SamplesPerPixel = CONFIGS[cfg][1], CONFIGS[cfg][2]
+        if scene == "book1":
+            cam.AspectRatio = 1.5
+        d = cam.derived()
+        key = f"{scene}:{d.width}x{d.height}x{d.spp_sqrt ** 2}"
+        raw = os.path.join(out_dir, f"{tag}_pmc_{cfg}.json")
+        with open(raw, "w") as f:
+            json.dump({"config": cfg, "key": key, "bench_args": bench_args, "kernels": res}, f,
+                      indent=1)
+        db[key] = {k: {kk: v for kk, v in e.items() if kk != "counters_per_launch"}
+                   for k, e in res.items()}
+        for e in db[key].values():
+            e["_source"] = f"profiles/{tag}_pmc_{cfg}.json"
+        with open(tpath, "w") as f:
+            json.dump(db, f, indent=1)
+        print(cfg, key, json.dumps(db[key].get("k_fused", {})), flush=True)
 
 
 if __name__ == "__main__":
