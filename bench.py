@@ -95,9 +95,11 @@ def cpu_baseline(tree, world, lights, cam, target_s):
     d = cam.derived()
     px_row = d.width * d.spp_sqrt ** 2
 
-    def sample(nthreads, seconds):
+    def sample(nthreads, seconds, k):
+        # calibrate on k rows spread over the image (row cost varies a lot: the
+        # Cornell light), then take every stride-th row for ~`seconds` of work
         _, st = pyoracle.render(tree, world, lights, cam, seed=1, threads=nthreads, rank=0,
-                                nranks=d.height, max_rows=1)
+                                nranks=max(1, d.height // k), max_rows=k)
         rate = st["samples"] / max(st["seconds"], 1e-6)
         rows_wanted = max(1, int(seconds * rate / px_row))
         stride = max(1, d.height // rows_wanted)
@@ -105,8 +107,8 @@ def cpu_baseline(tree, world, lights, cam, target_s):
                                 nranks=stride)
         return st, stride, len(range(0, d.height, stride))
 
-    st, stride, rows = sample(threads, target_s)
-    st1, stride1, rows1 = sample(1, target_s / 3)
+    st, stride, rows = sample(threads, target_s, 32)
+    st1, stride1, rows1 = sample(1, target_s / 3, 8)
     v16 = st["samples"] / st["seconds"] / 1e6
     v1 = st1["samples"] / st1["seconds"] / 1e6
     # configs[0]: C1 quads 400x400, 64 spp, one thread, the whole image

@@ -501,7 +501,8 @@ int flatten_scene(const Tree& t, int world, int lights, HostScene& out) {
     DevPerlin d{};
     for (int i = 0; i < 256; ++i)
       d.ranvec[i] = {(float)p.ranvec[i][0], (float)p.ranvec[i][1], (float)p.ranvec[i][2], 0};
-    memcpy(d.perm, p.perm, sizeof d.perm);
+    for (int a = 0; a < 3; ++a)  // values are 0..255 (checked at rt_tex_noise_tables)
+      for (int i = 0; i < 256; ++i) d.perm[a][i] = (uint8_t)p.perm[a][i];
     out.perlins.push_back(d);
   }
   // keep prim bounds for export, in the BVH's final ref order (set by build_bvh)

@@ -107,7 +107,7 @@ struct DevImage {
 
 struct DevPerlin {           // perlin.go:10-31
   F4 ranvec[256];
-  int32_t perm[3][256];
+  uint8_t perm[3][256];      // permutations of 0..255, one byte each
 };
 
 struct DevScene {
@@ -137,7 +137,8 @@ struct DevScene {
   const DevImage* images;
   const DevPerlin* perlins;
   int32_t brute_ax[3];  // record loop (TREE 0): axis-aligned pairs per normal axis, after
-  int32_t _pad_ax;      // the general pairs (host-grouped; rt_path.h brute_axis)
+                        // the general pairs (host-grouped; rt_path.h brute_axis)
+  int32_t n_perlins;    // perlin 0's tables are staged in LDS by the noise kernels
 };
 
 }  // namespace rt

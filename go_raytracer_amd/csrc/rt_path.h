@@ -573,17 +573,37 @@ RT_D void trace_media(const Params& P, f3 o, f3 d, float time, float tmin, uint3
 
 // ---------------------------------------------------------------- shading --
 // Texture.Value texture.go:10-125 (checker chains resolved iteratively)
-RT_D float perlin_noise(const DevPerlin& pl, f3 p) {  // perlin.go:34-54
+// Perlin tables of perlin 0 in LDS (kernels with FT_NOISE stage them at start,
+// stage_perlin): ranvec as float4 and the three byte permutations, the same layout
+// as DevPerlin.  The noise evaluation is 7 octaves x 8 lattice corners of dependent
+// table reads (book2's marble sphere, C4): from HBM/L2 they were latency-bound (C4
+// -23 % with texture evaluation ablated).  One code path serves both copies: the
+// tables are reached through a generic pointer (LDS for perlin 0, global for the
+// others), so the hardware routes each flat load (a second, address-space-specific
+// copy of the noise code doubled the kernel's spills).
+__shared__ DevPerlin g_perlin;
+
+// before the kernel's first __syncthreads (stage_nodes), every thread of the block
+RT_D void stage_perlin(const DevScene& sc) {
+  if (sc.n_perlins <= 0) return;
+  const F4* src = (const F4*)sc.perlins;
+  F4* dst = (F4*)&g_perlin;
+  for (int i = threadIdx.x; i < (int)(sizeof(DevPerlin) / 16); i += blockDim.x) dst[i] = src[i];
+}
+
+RT_D float perlin_noise(const DevPerlin* pl, f3 p) {  // perlin.go:34-54
   float fx = floorf(p.x), fy = floorf(p.y), fz = floorf(p.z);
   float u = p.x - fx, v = p.y - fy, w = p.z - fz;
   int i = (int)fx, j = (int)fy, k = (int)fz;
   float uu = u * u * (3 - 2 * u), vv = v * v * (3 - 2 * v), ww = w * w * (3 - 2 * w);
+  const int pi[2] = {pl->perm[0][i & 255], pl->perm[0][(i + 1) & 255]},
+            pj[2] = {pl->perm[1][j & 255], pl->perm[1][(j + 1) & 255]},
+            pk[2] = {pl->perm[2][k & 255], pl->perm[2][(k + 1) & 255]};
   float accum = 0.0f;
   for (int di = 0; di < 2; ++di)
     for (int dj = 0; dj < 2; ++dj)
       for (int dk = 0; dk < 2; ++dk) {
-        int idx = pl.perm[0][(i + di) & 255] ^ pl.perm[1][(j + dj) & 255] ^ pl.perm[2][(k + dk) & 255];
-        F4 g = pl.ranvec[idx];
+        const F4 g = pl->ranvec[pi[di] ^ pj[dj] ^ pk[dk]];
         f3 wt = mk3(u - (float)di, v - (float)dj, w - (float)dk);
         accum += ((float)di * uu + (float)(1 - di) * (1 - uu)) *
                  ((float)dj * vv + (float)(1 - dj) * (1 - vv)) *
@@ -591,8 +611,9 @@ RT_D float perlin_noise(const DevPerlin& pl, f3 p) {  // perlin.go:34-54
       }
   return accum;
 }
-RT_D float perlin_turb(const DevPerlin& pl, f3 p, int depth) {  // perlin.go:57-69
+RT_D float perlin_turb(const DevPerlin* pl, f3 p, int depth) {  // perlin.go:57-69
   float accum = 0.0f, weight = 1.0f;
+#pragma unroll 1  // unrolled, the scheduler hoists every octave's table reads
   for (int i = 0; i < depth; ++i) {
     accum += weight * perlin_noise(pl, p);
     weight *= 0.5f;
@@ -603,6 +624,9 @@ RT_D float perlin_turb(const DevPerlin& pl, f3 p, int depth) {  // perlin.go:57-
 
 template <uint32_t FT>
 RT_D f3 tex_value(const DevScene& sc, int tex, float u, float v, f3 p) {
+#ifdef ABL_NO_TEX
+  return xyz(sc.texs[tex].color);  // ablation build (timing only)
+#endif
   for (int guard = 0; guard < 64; ++guard) {
     const DevTexture T = sc.texs[tex];
     if (!HAS(FT_CHECKER | FT_IMAGE | FT_NOISE) || T.kind == RT_TEX_SOLID) return xyz(T.color);
@@ -628,18 +652,13 @@ RT_D f3 tex_value(const DevScene& sc, int tex, float u, float v, f3 p) {
       return mk3((float)px[0] * s, (float)px[1] * s, (float)px[2] * s);
     }
     if (!HAS(FT_NOISE)) return mk3(0, 0, 0);
-    // noise, texture.go:112-125
-    const DevPerlin& pl = sc.perlins[T.a];
-    float scale = T.color.w;
-    if (T.variant == RT_NOISE_MARBLE) {
-      float s = 0.5f * (1.0f + sinf(scale * p.z + 10.0f * perlin_turb(pl, p, 7)));
-      return mk3(s, s, s);
-    }
-    if (T.variant == RT_NOISE_TURBULENT) {
-      float s = perlin_turb(pl, p, 7);
-      return mk3(s, s, s);
-    }
-    float s = 0.5f * (1.0f + perlin_noise(pl, p * scale));
+    // noise, texture.go:112-125 (perlin 0 from its LDS copy when staged)
+    const DevPerlin* pl = (T.a == 0 && sc.n_perlins > 0) ? &g_perlin : sc.perlins + T.a;
+    const float scale = T.color.w;
+    float s;
+    if (T.variant == RT_NOISE_MARBLE) s = 0.5f * (1.0f + sinf(scale * p.z + 10.0f * perlin_turb(pl, p, 7)));
+    else if (T.variant == RT_NOISE_TURBULENT) s = perlin_turb(pl, p, 7);
+    else s = 0.5f * (1.0f + perlin_noise(pl, p * scale));
     return mk3(s, s, s);
   }
   return mk3(0, 0, 0);
@@ -839,7 +858,8 @@ struct Path {
   uint32_t chunk, j, k, nst, flags;
   uint32_t gpix, s0;  // global pixel and first sample of the chunk (chunk_ids, cached)
   f3 pend, pre;
-  uint32_t segs, pushes;  // per-lane statistics (fused kernel)
+  uint32_t segs;    // world.Hit calls of this lane (statistics)
+  uint32_t pushes;  // clamp weights stored (statistics, RT_COUNT_PUSHES builds only)
 };
 
 template <bool SOA>
@@ -875,14 +895,23 @@ struct WStack {
       q[nlds * 256] = v.y;
       q[2 * nlds * 256] = v.z;
     } else {
-      st_glb(P.stack + (size_t)(k - nlds) * P.P + slot, v);
+      st_glb(P.stack + hbm_index(P, slot, k), v);
     }
+  }
+  // HBM entries: [entry][slot] (a wave's lanes at one depth coalesce) or, with
+  // WSTACK_SLOT_MAJOR, [slot][entry] (one lane's pushes share cache lines)
+  RT_D size_t hbm_index(const Params& P, uint32_t slot, uint32_t k) const {
+#ifdef WSTACK_SLOT_MAJOR
+    return (size_t)slot * (P.max_depth + 1) + (k - nlds);
+#else
+    return (size_t)(k - nlds) * P.P + slot;
+#endif
   }
   // backward clamp fold over entries nst-1 .. 0 (camera.go:328-330): the HBM
   // entries (rare) one by one, the LDS entries read together and applied unrolled
   RT_D f3 fold(const Params& P, uint32_t slot, uint32_t nst, f3 L) const {
     for (int k = (int)nst - 1; k >= nlds; --k)
-      L = clamp_contribution(xyz(ld_glb(P.stack + (size_t)(k - nlds) * P.P + slot)) * L, P.maxc);
+      L = clamp_contribution(xyz(ld_glb(P.stack + hbm_index(P, slot, (uint32_t)k))) * L, P.maxc);
     if (nlds > 0 && nst > 0) {
       const lds_f32* q = (const lds_f32*)lds;
       f3 e[kLdsWMax];
@@ -1100,7 +1129,9 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
           f3 pv = get_pend<SOA>(P, slot, s);
           ws.put(P, slot, s.nst, {pv.x, pv.y, pv.z, 0.0f});
           ++s.nst;
-          ++s.pushes;
+#ifdef RT_COUNT_PUSHES
+          ++s.pushes;  // a per-lane counter costs the fused kernels a VGPR: opt-in
+#endif
         }
         set_pend<SOA>(P, slot, s, weight);
         s.flags |= F_PEND;

@@ -56,7 +56,11 @@ RT_D void record_trace(const Params& P, const Path& s, const Hit& best) {
 // media + debug trace on top of the world closest hit, camera.go:300
 template <uint32_t FT>
 RT_D void finish_hit(const Params& P, const Path& s, Hit& best) {
+#ifdef ABL_NO_MEDIA
+  if (false)
+#else
   if (HAS(FT_MEDIA) && P.sc.n_media > 0)
+#endif
     trace_media(P, s.o, s.d, s.time, 0.001f, s.gpix, s.s0 + s.j, s.k, best);
   if (P.trace) record_trace(P, s, best);
 }
@@ -103,6 +107,8 @@ __global__ __launch_bounds__(256) void k_extend(Params P, int it) {
 
 __global__ __launch_bounds__(256) void k_shade(Params P, int it) {
   __shared__ uint32_t wave_cnt[4], wave_base[4], block_base;
+  stage_perlin(P.sc);
+  __syncthreads();
   const uint32_t sel = (uint32_t)it & 1u;
   uint32_t cnt[kXcd];
   uint32_t n = 0;
@@ -199,6 +205,12 @@ constexpr int fused_waves(uint32_t ft, int tree = 4) {
 #ifndef MESH_SHORT
 #define MESH_SHORT kShortStack
 #endif
+#ifndef TEX_SHORT
+#define TEX_SHORT kShortStack
+#endif
+#ifndef TEX_WLDS
+#define TEX_WLDS 4  // book2's set: room for the staged perlin tables at 4 waves/SIMD
+#endif
 #ifndef ALL_WLDS
 #define ALL_WLDS 4  // 6 pushed the C3-size trees out of the 3-wave LDS budget
 #endif
@@ -206,6 +218,7 @@ constexpr int fused_wlds(uint32_t ft, int tree = 4) {
   return ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? MESH_WLDS
          : (ft == 0u && tree != 0)                                  ? 4
          : ft == FT_ALL                                             ? ALL_WLDS
+         : ft == (FT_SPHERE | FT_METAL | FT_DIEL | FT_MEDIA | FT_IMAGE | FT_NOISE) ? TEX_WLDS
                                                                     : kLdsWMax;
 }
 // short traversal stack: none for the record loop, 6 entries for the lean set
@@ -214,11 +227,13 @@ constexpr int fused_short(uint32_t ft, int tree = 4) {
   return tree == 0                                                    ? 0
          : ft == 0u                                                   ? kShortStackMin
          : ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? MESH_SHORT
+         : ft == (FT_SPHERE | FT_METAL | FT_DIEL | FT_MEDIA | FT_IMAGE | FT_NOISE) ? TEX_SHORT
                                                                       : kShortStack;
 }
-// + 24 B per lane of chunk sums (SampleAcc)
+// + 24 B per lane of chunk sums (SampleAcc) + the perlin tables of noise kernels
 constexpr unsigned fused_static_lds(uint32_t ft, int tree = 4) {
-  return (unsigned)(fused_short(ft, tree) * 4 + fused_wlds(ft, tree) * 12 + 24) * 256u;
+  return (unsigned)(fused_short(ft, tree) * 4 + fused_wlds(ft, tree) * 12 + 24) * 256u +
+         ((ft & FT_NOISE) ? 256u * 16u + 768u : 0u);
 }
 // TREE: 4 = BVH4, 2 = BVH2, 0 = no tree (every record tested, tiny scenes)
 template <bool LDS, uint32_t FT, int TREE>
@@ -228,14 +243,19 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
   __shared__ float lw[3 * fused_wlds(FT, TREE) * 256];
   __shared__ unsigned long long lacc[3 * 256];  // per-lane chunk sums (SampleAcc)
   for (int ch = 0; ch < 3; ++ch) lacc[ch * 256 + threadIdx.x] = 0ull;
+  if constexpr (HAS(FT_NOISE)) stage_perlin(P.sc);  // before stage_nodes' barrier
   const bool recs_lds = LDS && stage_nodes(P, lnodes, TREE == 4 ? 8 : 4);
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;  // weight-stack column
   const TravStack ts = {&lstack[threadIdx.x], P.ostack + slot, P.stack_cols, fused_short(FT, TREE)};
   const WStack ws = {&lw[threadIdx.x], fused_wlds(FT, TREE)};
   const SampleAcc sa = {&lacc[threadIdx.x]};
   Path s;
-  s.segs = 0;
   s.pushes = 0;
+#ifdef RT_WAVE_SEGS
+  uint32_t wave_segs = 0;  // segments shaded by this wave (wave-uniform: no VGPR)
+#else
+  s.segs = 0;
+#endif
   Trav tr;
   tr.cur = TRAV_DONE;
   bool has = false;
@@ -265,20 +285,28 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
     const uint32_t n_ready = (uint32_t)__popcll(__ballot(ready));
     const bool busy = __any(has && !ready);
     if (n_ready >= P.shade_min || !busy) {
+#ifdef RT_WAVE_SEGS
+      wave_segs += n_ready;
+#endif
       if (ready) {
         Hit best = tr.best;
         finish_hit<FT>(P, s, best);
+#ifndef RT_WAVE_SEGS
         ++s.segs;
+#endif
         if (shade_core<false, FT>(P, slot, s, best, ws, sa) == OUT_NEED_CHUNK) has = false;
         else trav_init(P.sc, s.d, tr);
       }
     }
   }
-  uint32_t segs = s.segs, pushes = s.pushes;
-  for (int off = 32; off > 0; off >>= 1) {
-    segs += __shfl_xor(segs, off);
-    pushes += __shfl_xor(pushes, off);
-  }
+#ifdef RT_WAVE_SEGS
+  const uint32_t segs = wave_segs;
+#else
+  uint32_t segs = s.segs;
+  for (int off = 32; off > 0; off >>= 1) segs += __shfl_xor(segs, off);
+#endif
+  uint32_t pushes = s.pushes;
+  for (int off = 32; off > 0; off >>= 1) pushes += __shfl_xor(pushes, off);
   if (lane_id() == 0) {
     atomicAdd(&P.ctr->segments, (unsigned long long)segs);
     atomicAdd(&P.ctr->pushes, (unsigned long long)pushes);
@@ -620,6 +648,7 @@ static int upload_scene(const Scene* s, DeviceScene* ds) {
   d.medium_draws = h.medium_draws;
   d.n_lights = (int32_t)h.lights.size();
   d.n_refs = (int32_t)h.refs.size();
+  d.n_perlins = (int32_t)h.perlins.size();
   return RT_OK;
 }
 

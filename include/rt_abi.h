@@ -332,7 +332,7 @@ typedef struct {
 typedef struct {
   uint64_t samples;      /* W*rows*spp_sqrt^2 rendered by this call */
   uint64_t segments;     /* closest-hit queries (world.Hit calls, camera.go:300) */
-  uint64_t stack_pushes; /* clamp-vertex weights spilled to HBM */
+  uint64_t stack_pushes; /* clamp-vertex weights stored (0 unless built with RT_COUNT_PUSHES) */
   uint64_t extend_rays;  /* total rays processed by extend launches */
   uint64_t shade_rays;
   double ms_total;       /* render wall time (host, incl. sync) */
