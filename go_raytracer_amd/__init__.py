@@ -513,6 +513,14 @@ def demo_scene(name, seed=1, asset_dir=None):
     return t, Camera.from_c(cam), w.value, l.value
 
 
+def substitute_mesh_obj(nu=0, nv=0):
+    """The "model" scene's dragon.obj substitute as OBJ bytes (rt_substitute_mesh_obj)."""
+    n = check(int(lib().rt_substitute_mesh_obj(nu, nv, None, 0)))
+    buf = C.create_string_buffer(n)
+    check(int(lib().rt_substitute_mesh_obj(nu, nv, buf, n)))
+    return buf.raw[:n]
+
+
 def quantize(rgb):
     """PrintColor (vec/color.go:23-46) on a float32 [..., 3] image -> uint8."""
     a = np.ascontiguousarray(rgb, dtype=np.float32)

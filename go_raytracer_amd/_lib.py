@@ -59,7 +59,7 @@ class RtSceneInfo(C.Structure):
         "n_spheres", "n_quads", "n_triangles", "n_world_prims", "n_media",
         "n_lights", "n_bvh_nodes", "bvh_depth", "max_leaf", "n_materials",
         "n_textures", "n_images", "n_perlins", "medium_draws")] + [
-        ("device_bytes", C.c_int64), ("features", C.c_int32), ("_pad", C.c_int32)]
+        ("device_bytes", C.c_int64), ("features", C.c_int32), ("bvh_builder", C.c_int32)]
 
 
 class RtRenderOpts(C.Structure):
@@ -191,6 +191,7 @@ SIGNATURES = {
     "rt_demo_scene": (_I, [_P, C.c_char_p, C.c_char_p, C.POINTER(RtCamera), C.POINTER(_I),
                            C.POINTER(_I)]),
     "rt_demo_scene_name": (_I, [_I, C.POINTER(C.c_char_p)]),
+    "rt_substitute_mesh_obj": (C.c_int64, [_I, _I, C.c_void_p, C.c_int64]),
     "rt_device_count": (_I, []),
 }
 

@@ -507,9 +507,22 @@ int flatten_scene(const Tree& t, int world, int lights, HostScene& out) {
   }
   // keep prim bounds for export, in the BVH's final ref order (set by build_bvh)
   t0 = std::chrono::steady_clock::now();
-  rc = build_bvh(out, f.lo, f.hi, f.world_refs);
+  // large scenes: PLOC on the GPU (rt_build.hip) when a device is present
+  const char* bsel = getenv("RT_BVH_BUILDER");
+  const std::string builder = bsel ? bsel : "auto";
+  const char* bmin = getenv("RT_BVH_DEVICE_MIN");
+  const size_t dev_min = bmin && *bmin ? (size_t)atol(bmin) : (size_t)65536;
+  const bool on_device =
+      f.world_refs.size() >= 2 &&
+      (builder == "device" || (builder == "auto" && f.world_refs.size() >= dev_min)) &&
+      bvh_device_available();
+  if (builder == "device" && !on_device && f.world_refs.size() >= 2)
+    return set_error(RT_ERR_DEVICE, "RT_BVH_BUILDER=device but no HIP device is available");
+  out.bvh_builder = on_device ? 1 : 0;
+  rc = on_device ? build_bvh_device(out, f.lo, f.hi, f.world_refs, 0)
+                 : build_bvh(out, f.lo, f.hi, f.world_refs);
   if (timing)
-    fprintf(stderr, "[rt] build_bvh %.3f s\n",
+    fprintf(stderr, "[rt] build_bvh (%s) %.3f s\n", on_device ? "device" : "host",
             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
   return rc;
 }

@@ -128,6 +128,7 @@ int rt_scene_info_get(const rt_scene* sc, rt_scene_info* o) {
   b += h.images.size() * sizeof(rt::DevImage) + h.perlins.size() * sizeof(rt::DevPerlin);
   o->device_bytes = b;
   o->features = (int32_t)rt::scene_features(h);
+  o->bvh_builder = h.bvh_builder;
   return RT_OK;
 }
 

@@ -16,6 +16,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -444,9 +445,16 @@ int model(rt_tree* t, const char* asset_dir, rt_camera* c, int* world_out, int* 
     fclose(f);
     CHECK(rt_load_obj(t, path.c_str(), &opt, &mdl, &lights, nullptr));
   } else {
+    const bool timing = getenv("RT_TIMING") != nullptr;
+    auto t0 = std::chrono::steady_clock::now();
     std::string obj = substitute_dragon_obj(nu < 0 ? 2048 : nu, nv < 0 ? 256 : nv);
+    auto t1 = std::chrono::steady_clock::now();
     CHECK(rt_load_obj_memory(t, obj.data(), obj.size(), nullptr, 0, "dragon.obj", &opt, &mdl,
                              &lights, nullptr));
+    if (timing)
+      fprintf(stderr, "[rt] substitute OBJ text %.3f s (%zu bytes), LoadObj %.3f s\n",
+              std::chrono::duration<double>(t1 - t0).count(), obj.size(),
+              std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count());
   }
   CHECK(rt_list_add(t, world, rt_rotate_y(t, mdl, 180)));
   // the sun joins the model's light list (main.go:385-391)
@@ -473,6 +481,17 @@ const char* kNames[] = {nullptr, "book1", "book2", "book3", "simple_light",
 }  // namespace
 
 extern "C" {
+
+int64_t rt_substitute_mesh_obj(int nu, int nv, char* out, int64_t cap) {
+  const std::string obj = substitute_dragon_obj(nu > 0 ? nu : 2048, nv > 0 ? nv : 256);
+  if (out) {
+    if (cap < (int64_t)obj.size())
+      return set_error(RT_ERR_INVALID, "rt_substitute_mesh_obj: buffer of %lld < %zu bytes",
+                       (long long)cap, obj.size());
+    memcpy(out, obj.data(), obj.size());
+  }
+  return (int64_t)obj.size();
+}
 
 int rt_demo_scene_name(int s, const char** name_out) {
   if (!name_out) return set_error(RT_ERR_INVALID, "rt_demo_scene_name: null");

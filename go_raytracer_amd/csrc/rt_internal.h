@@ -64,6 +64,7 @@ struct HostScene {
   int32_t n_world_prims = 0;
   int32_t bvh_depth = 0;
   int32_t max_leaf = 0;
+  int32_t bvh_builder = 0;  // 0 host binned SAH, 1 device PLOC
 };
 
 struct DeviceScene;  // defined in the HIP translation unit
@@ -106,6 +107,10 @@ int flatten_scene(const Tree& t, int world, int lights, HostScene& out);
 // host_bvh.cpp
 int build_bvh(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi,
               const std::vector<uint32_t>& prims);
+// rt_build.hip: the same outputs as build_bvh, built by PLOC on `device`
+int build_bvh_device(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi,
+                     const std::vector<uint32_t>& prims, int device);
+bool bvh_device_available();
 // host_scene.cpp: RT_FT_* features a flattened scene needs
 uint32_t scene_features(const HostScene& h);
 // rt_render.hip

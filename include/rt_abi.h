@@ -266,7 +266,10 @@ int rt_camera_derive(const rt_camera* cam, rt_camera_derived* out);
 typedef struct rt_scene rt_scene;
 
 /* Flatten world/lights (transforms baked, media separated, light table built)
- * and build the device BVH.  Host-only: no GPU needed.  lights may be -1. */
+ * and build the device BVH (BuildBVH bvh.go:21-61 + the world list).  Scenes of
+ * >= 65536 world prims build it on HIP device 0 (PLOC, DESIGN.md "BVH") when one is
+ * present, otherwise with the host binned-SAH builder; RT_BVH_BUILDER=host|device
+ * overrides, RT_BVH_DEVICE_MIN moves the threshold.  lights may be -1. */
 int rt_scene_create(const rt_tree* t, int world, int lights, rt_scene** out);
 int rt_scene_destroy(rt_scene* s);
 
@@ -278,7 +281,7 @@ typedef struct {
   int32_t medium_draws; /* total free-flight draws per vertex */
   int64_t device_bytes; /* scene bytes uploaded to HBM */
   int32_t features;     /* RT_FT_* bits the scene needs (selects the fused kernel) */
-  int32_t _pad;
+  int32_t bvh_builder;  /* 0: host binned SAH, 1: device PLOC (rt_scene_create) */
 } rt_scene_info;
 
 /* scene features (rt_scene_info.features, rt_stats.kernel_features) */
@@ -416,6 +419,11 @@ int64_t rt_format_ppm_device(const float* rgb_dev, int w, int h, char* out_dev, 
 int rt_demo_scene(rt_tree* t, const char* name, const char* asset_dir, rt_camera* cam,
                   int* world, int* lights);
 int rt_demo_scene_name(int s_number, const char** name_out);
+/* The "model" scene's substitute for dragon.obj (absent from the reference) as OBJ
+ * text: nu x nv grid of a torus-knot tube (nu, nv <= 0: 2048 x 256 = 1M triangles).
+ * Returns the byte count; call with out = NULL to size.  Writing it to
+ * <asset_dir>/dragon.obj lets "model" load it from disk like the real mesh. */
+int64_t rt_substitute_mesh_obj(int nu, int nv, char* out, int64_t cap);
 
 /* Number of HIP devices visible (0 on a CPU-only host; never aborts). */
 int rt_device_count(void);

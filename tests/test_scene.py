@@ -52,37 +52,39 @@ def test_scene_is_pure_function_of_seed(rt):
     assert fingerprint(1) != fingerprint(2)
 
 
-@pytest.mark.parametrize("name", ["cornell", "book1", "book2", "quads", "model:96x24"])
-def test_bvh_invariants(rt, name):
-    t, cam, w, l = rt.demo_scene(name)
-    with rt.Scene(t, w, l) as sc:
-        nodes, refs, root, bounds = sc.export_bvh()
-        i = sc.info()
+def bvh_invariants(sc):
+    """Every world prim is in exactly one leaf and every box contains what is below
+    it (the exported BVH2; the BVH4 shares its leaves and boxes)."""
+    nodes, refs, root, bounds = sc.export_bvh()
+    i = sc.info()
     n = len(refs)
     assert n == i["n_world_prims"]
     seen = np.zeros(n, np.int32)
-
-    def leaf(code):
-        return (code >> 4) & 0x7FFFFFF, (code & 15) + 1
-
-    def check(code, lo, hi):
+    stack = [(root, np.full(3, -np.inf, np.float32), np.full(3, np.inf, np.float32))]
+    while stack:  # iterative: device-built trees of big meshes are deep
+        code, lo, hi = stack.pop()
         if code & 0x80000000:
-            first, cnt = leaf(code)
+            first, cnt = (code >> 4) & 0x7FFFFFF, (code & 15) + 1
             seen[first:first + cnt] += 1
             b = bounds[first:first + cnt]
             assert (b[:, :3] >= lo - 1e-6).all() and (b[:, 3:] <= hi + 1e-6).all()
-            return
+            continue
         nd = nodes[code]
         c0 = int(nd[3:4].view(np.uint32)[0])
         c1 = int(nd[7:8].view(np.uint32)[0])
         for c, (blo, bhi) in ((c0, (nd[0:3], nd[4:7])), (c1, (nd[8:11], nd[12:15]))):
             assert (blo >= lo - 1e-6).all() and (bhi <= hi + 1e-6).all()
-            check(c, blo, bhi)
-
-    big = np.full(3, np.inf, np.float32)
-    check(root, -big, big)
+            stack.append((c, blo, bhi))
     assert (seen == 1).all(), "every world prim is referenced by exactly one leaf"
     assert i["max_leaf"] <= 16
+    return nodes, refs, bounds
+
+
+@pytest.mark.parametrize("name", ["cornell", "book1", "book2", "quads", "model:96x24"])
+def test_bvh_invariants(rt, name):
+    t, cam, w, l = rt.demo_scene(name)
+    with rt.Scene(t, w, l) as sc:
+        bvh_invariants(sc)
 
 
 def test_light_table_matches_nested_picks(rt):
