@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stddef.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -509,7 +510,11 @@ static int ensure_scene(Scene* s, int device, DeviceScene** out) {
   }
   DeviceScene* ds = new DeviceScene();
   ds->device = device;
+  const auto t0 = std::chrono::steady_clock::now();
   const int rc = upload_scene(s, ds);
+  if (getenv("RT_TIMING"))
+    fprintf(stderr, "[rt] scene upload to device %d %.3f s\n", device,
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
   if (rc != RT_OK) {
     delete ds;
     return rc;
@@ -550,9 +555,13 @@ static int upload_scene(const Scene* s, DeviceScene* ds) {
   UP(h.tri, tri);
   UP(h.tri_attr, tri_attr);
   UP(h.nodes4, nodes);
-  if ((rc = upload(ds, h.nodes, &ds->nodes2)) != RT_OK) return rc;
+  // the BVH2 and the record-loop pairs serve tiny scenes only (render_impl's tree
+  // choice: <= 64 leaf entries); a 1M-triangle scene would upload 64 MB of BVH2
+  const size_t tiny = (size_t)std::max(64, env_int("RT_BRUTE_MAX", kBruteMax));
+  const bool small = h.refs.size() <= tiny;
+  if (small && (rc = upload(ds, h.nodes, &ds->nodes2)) != RT_OK) return rc;
   ds->root2 = h.root;
-  ds->n_nodes2 = (int32_t)(h.nodes.size() / 4);
+  ds->n_nodes2 = small ? (int32_t)(h.nodes.size() / 4) : 0;
   UP(h.refs, refs);
   {
     std::vector<F4> recs, lrecs;
@@ -560,6 +569,7 @@ static int upload_scene(const Scene* s, DeviceScene* ds) {
     UP(recs, leafprims);
     build_light_records(h, lrecs);
     UP(lrecs, light_recs);
+    if (!small) goto records_done;
     // record-loop order: largest surface first, so the closest hit tends to be found
     // early and later records fail the interval test before their slower half
     std::vector<size_t> ord(h.refs.size());
@@ -633,6 +643,7 @@ static int upload_scene(const Scene* s, DeviceScene* ds) {
     ds->brute_slots = slots.size();
     if ((rc = upload(ds, pairs, &ds->brute_pairs)) != RT_OK) return rc;
   }
+records_done:
   UP(h.media, media);
   UP(h.medium_refs, medium_refs);
   UP(h.lights, lights);
