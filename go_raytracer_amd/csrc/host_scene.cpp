@@ -89,6 +89,7 @@ int rt_scene_create(const rt_tree* t, int world, int lights, rt_scene** out) {
     delete s;
     return rc;
   }
+  s->s.h.features = rt::scene_features(s->s.h);  // walks every prim: once, not per render
   *out = s;
   return RT_OK;
 }
@@ -127,7 +128,7 @@ int rt_scene_info_get(const rt_scene* sc, rt_scene_info* o) {
   b += h.texs.size() * sizeof(rt::DevTexture) + h.texels.size();
   b += h.images.size() * sizeof(rt::DevImage) + h.perlins.size() * sizeof(rt::DevPerlin);
   o->device_bytes = b;
-  o->features = (int32_t)rt::scene_features(h);
+  o->features = (int32_t)h.features;
   o->bvh_builder = h.bvh_builder;
   return RT_OK;
 }

@@ -65,6 +65,7 @@ struct HostScene {
   int32_t bvh_depth = 0;
   int32_t max_leaf = 0;
   int32_t bvh_builder = 0;  // 0 host binned SAH, 1 device PLOC
+  uint32_t features = 0;    // scene_features(), computed once by rt_scene_create
 };
 
 struct DeviceScene;  // defined in the HIP translation unit
