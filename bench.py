@@ -54,8 +54,9 @@ EXTRA = [("C3", "book1", 1200, 512, 3),   # main.go:19-91, aspect 1.5 -> 1200x80
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    # 64 steps of C2: a ~3 s timed region (the driver samples GPU activity during it)
+    ap.add_argument("--steps", type=int, default=64)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--scene", default="cornell")
     ap.add_argument("--width", type=int, default=800)
     ap.add_argument("--spp", type=int, default=1024)

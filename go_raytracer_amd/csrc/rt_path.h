@@ -87,6 +87,36 @@ RT_D uint32_t pack_path(uint32_t j, uint32_t k, uint32_t nst, uint32_t flags) {
 }
 
 RT_D uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+// Debug build (-DRT_PHASES, tools/phase_probe.py): shader-clock cycles each wave
+// spends per phase of the fused loop, accumulated by lane 0 in LDS and written with
+// the RT_WAVE_TIMES record.  Timing perturbs the kernel (s_memtime waits): use the
+// shares, not the absolute cycles.
+enum { PH_GRAB, PH_TRAV, PH_MEDIA, PH_SHADE, PH_TEX, PH_LIGHT, PH_TERM, PH_LOOP,
+       PH_TRAV_LANES, PH_TRAV_ROUNDS, PH_SHADE_LANES, PH_SHADE_ROUNDS, PH_STEP_LANES,
+       PH_STEP_WAVE, PH_N = 14 };
+constexpr int kWaveRec = 4 + PH_N;  // {start, end, segments, pad, phases...} per wave
+#ifdef RT_PHASES
+__shared__ unsigned long long g_ph[4][PH_N];
+RT_D unsigned long long ph_now() { return __builtin_readcyclecounter(); }
+RT_D void ph_acc(int i, unsigned long long v) {  // first active lane (divergent code too)
+  if (lane_id() == (uint32_t)(__ffsll((long long)__ballot(1)) - 1)) g_ph[threadIdx.x >> 6][i] += v;
+}
+#define PH_T(v) const unsigned long long v = ::rt::ph_now()
+#define PH_ADD(i, v) ::rt::ph_acc(i, ::rt::ph_now() - (v))
+#define PH_CNT(i, n) ::rt::ph_acc(i, (unsigned long long)(n))
+// traversal steps: summed over the lanes, and the wave's maximum (loop trips)
+RT_D void ph_steps(int n) {
+  atomicAdd(&g_ph[threadIdx.x >> 6][PH_STEP_LANES], (unsigned long long)n);
+  int m = n;
+  for (int off = 32; off > 0; off >>= 1) m = max(m, __shfl_xor(m, off));
+  ph_acc(PH_STEP_WAVE, (unsigned long long)m);
+}
+#else
+#define PH_T(v)
+#define PH_ADD(i, v)
+#define PH_CNT(i, n)
+#endif
 RT_D uint32_t prefix_count(unsigned long long m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -239,7 +269,7 @@ RT_D void trav_init(const DevScene& sc, f3 d, Trav& tr) {
 // LDS instantiation: lnodes holds the node array and, when recs_lds, the leaf
 // records right after it (uniform flag: both load forms exist, one runs)
 template <bool LDS, uint32_t FT, bool W4 = true>
-RT_D void trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const TravStack& stack,
+RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const TravStack& stack,
                      f3 o, f3 d, float time, float tmin, Trav& tr, int budget) {
   uint32_t cur = tr.cur;
   int sp = tr.sp;
@@ -258,7 +288,8 @@ RT_D void trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const 
     }
   };
   const f3 inv = tr.inv;
-  for (int n = 0; n < budget && cur != TRAV_DONE; ++n) {
+  int n = 0;
+  for (; n < budget && cur != TRAV_DONE; ++n) {
     if (!W4 && !(cur & LEAF_BIT)) {
       // BVH2 node (tiny scenes, see render_impl): both child boxes, nearer first
       const F4* g = LDS ? lnodes + 4 * cur : sc.nodes + 4 * (size_t)cur;
@@ -359,6 +390,7 @@ RT_D void trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const 
   tr.cur = cur;
   tr.sp = sp;
   tr.top = top;
+  return n;
 }
 
 // Tiny scenes: every leaf record, in order, from the LDS cache (or through the
@@ -1099,7 +1131,10 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
         weight = mk3(1, 1, 1);
       } else {  // lambertian materials.go:45-57 / isotropic :157-177 + mixture pdf.go:58-74
         const bool iso = HAS(FT_MEDIA) && M.kind == RT_MAT_ISOTROPIC;
+        PH_T(t_tex);
         f3 att = tex_value<FT>(sc, M.tex, u, v, p);
+        PH_ADD(PH_TEX, t_tex);
+        PH_T(t_light);
         Onb b;
         if (!iso) b = make_onb(n);
         if (rt_unit_f(r.v[0]) < 0.5f) {
@@ -1120,6 +1155,7 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
           spdf = ct < 0.0f ? 0.0f : ct * kInvPi;
         }
         float pdf = 0.5f * lights_pdf<FT>(sc, p, ndir) + 0.5f * bsdf_pdf;
+        PH_ADD(PH_LIGHT, t_light);
         weight = (att * spdf) * rcp(pdf);
         clamp_vertex = true;
       }
@@ -1156,6 +1192,7 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
     }
   }
   // ---- termination: backward clamp fold (camera.go:316, :328-330)
+  PH_T(t_term);
   f3 L = lterm;
   const bool zero = lterm.x == 0.0f && lterm.y == 0.0f && lterm.z == 0.0f;
   if (!(zero && !(s.flags & F_NONFINITE))) {
@@ -1171,9 +1208,11 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
     if (!have_rcam)  // a miss, or the depth limit: the camera draw is made here
       rcam = rt_rng_draw(P.seed, s.gpix, s.s0 + s.j + 1, RT_STREAM_CAMERA);
     next_sample<SOA>(P, slot, s, s.j + 1, rcam);
+    PH_ADD(PH_TERM, t_term);
     return OUT_ALIVE;
   }
   sa.flush(P, s.chunk);
+  PH_ADD(PH_TERM, t_term);
   return OUT_NEED_CHUNK;
 }
 

@@ -266,22 +266,39 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
   // to step_budget traversal steps; lanes whose traversal is done are shaded
   // together once at least shade_min of them wait (or nothing else traverses),
   // so traversal divergence costs idle lanes only until the next round.
+#ifdef RT_PHASES
+  if (threadIdx.x < 4 * PH_N) (&g_ph[0][0])[threadIdx.x] = 0ull;
+  __syncthreads();
+#endif
+  PH_T(t_loop);
   for (;;) {
+    PH_T(t_grab);
     const uint32_t c = grab_chunk(P, b, !has);
     if (c != 0xFFFFFFFFu) {
       start_sample<false>(P, slot, s, c, 0);
       trav_init(P.sc, s.d, tr);
       has = true;
     }
+    PH_ADD(PH_GRAB, t_grab);
     if (!__any(has)) break;
+    PH_T(t_trav);
     if (has && tr.cur != TRAV_DONE)
     {
+      PH_CNT(PH_TRAV_LANES, __popcll(__ballot(1)));
+      PH_CNT(PH_TRAV_ROUNDS, 1);
       if constexpr (TREE == 0)
         trav_brute<FT, !LDS>(P.sc, lnodes, s.o, s.d, s.time, 0.001f, tr);
       else
-        trav_steps<LDS, FT, TREE == 4>(P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, tr,
-                                       P.step_budget);
+      {
+        const int nsteps = trav_steps<LDS, FT, TREE == 4>(P.sc, lnodes, recs_lds, ts, s.o, s.d,
+                                                          s.time, 0.001f, tr, P.step_budget);
+#ifdef RT_PHASES
+        ph_steps(nsteps);
+#endif
+        (void)nsteps;
+      }
     }
+    PH_ADD(PH_TRAV, t_trav);
     const bool ready = has && tr.cur == TRAV_DONE;
     const uint32_t n_ready = (uint32_t)__popcll(__ballot(ready));
     const bool busy = __any(has && !ready);
@@ -290,16 +307,23 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
       wave_segs += n_ready;
 #endif
       if (ready) {
+        PH_CNT(PH_SHADE_LANES, n_ready);
+        PH_CNT(PH_SHADE_ROUNDS, 1);
+        PH_T(t_media);
         Hit best = tr.best;
         finish_hit<FT>(P, s, best);
+        PH_ADD(PH_MEDIA, t_media);
 #ifndef RT_WAVE_SEGS
         ++s.segs;
 #endif
+        PH_T(t_shade);
         if (shade_core<false, FT>(P, slot, s, best, ws, sa) == OUT_NEED_CHUNK) has = false;
         else trav_init(P.sc, s.d, tr);
+        PH_ADD(PH_SHADE, t_shade);
       }
     }
   }
+  PH_ADD(PH_LOOP, t_loop);
 #ifdef RT_WAVE_SEGS
   const uint32_t segs = wave_segs;
 #else
@@ -313,9 +337,16 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
     atomicAdd(&P.ctr->pushes, (unsigned long long)pushes);
     if (P.wave_times) {
       const size_t w = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-      P.wave_times[3 * w] = t_start;
-      P.wave_times[3 * w + 1] = wall_clock64();
-      P.wave_times[3 * w + 2] = segs;
+      unsigned long long* rec = P.wave_times + kWaveRec * w;
+      rec[0] = t_start;
+      rec[1] = wall_clock64();
+      rec[2] = segs;
+      rec[3] = 0ull;
+#ifdef RT_PHASES
+      for (int i = 0; i < PH_N; ++i) rec[4 + i] = g_ph[threadIdx.x >> 6][i];
+#else
+      for (int i = 0; i < PH_N; ++i) rec[4 + i] = 0ull;
+#endif
     }
   }
 }
@@ -1054,12 +1085,13 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
       if ((rc = next_event(&e0)) || (rc = next_event(&e1))) return rc;
       HIP_OK(hipEventRecord(e0, stream));
     }
-    // debug: per-wave start/end clocks (100 MHz) + chunks -> binary file RT_WAVE_TIMES
+    // debug: per-wave start/end clocks (100 MHz), segments and (RT_PHASES builds) phase
+    // cycles -> binary file RT_WAVE_TIMES, kWaveRec u64 per wave
     const char* wt_path = getenv("RT_WAVE_TIMES");
     unsigned long long* wt = nullptr;
     const size_t n_waves = (size_t)fused_blocks * 4;
     if (wt_path && *wt_path) {
-      HIP_OK(hipMalloc(&wt, 3 * n_waves * sizeof(unsigned long long)));
+      HIP_OK(hipMalloc(&wt, kWaveRec * n_waves * sizeof(unsigned long long)));
       p.wave_times = wt;
     }
     void* args[] = {&p};
@@ -1076,7 +1108,7 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     }
     p.n_chunks = n_chunks;
     if (wt) {
-      std::vector<unsigned long long> h(3 * n_waves);
+      std::vector<unsigned long long> h(kWaveRec * n_waves);
       HIP_OK(hipMemcpyAsync(h.data(), wt, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost, stream));
       HIP_OK(hipStreamSynchronize(stream));
       HIP_OK(hipFree(wt));

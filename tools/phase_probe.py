@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Where the fused kernel's waves spend their cycles (dev tool).  Needs a library
+built with -DRT_PHASES (tools/build_variant.sh phases -DRT_PHASES; run with
+RT_AMD_LIB=go_raytracer_amd/build_abl/phases/librt_amd.so).
+usage: phase_probe.py scene width spp  -> one JSON line: phase shares of the loop's
+cycles, traversal/shading lane utilisation"""
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import go_raytracer_amd as rt  # noqa: E402
+
+NAMES = ["grab", "trav", "media", "shade", "tex", "light", "term", "loop",
+         "trav_lanes", "trav_rounds", "shade_lanes", "shade_rounds", "step_lanes", "step_wave"]
+scene, width, spp = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+t, cam, w, l = rt.demo_scene(scene)
+cam.Width = width
+if scene == "book1":
+    cam.AspectRatio = 1.5
+path = "/tmp/phase_times.bin"
+with rt.Scene(t, w, l) as sc:
+    cam.SamplesPerPixel = 1
+    sc.render(cam)
+    cam.SamplesPerPixel = spp
+    os.environ["RT_WAVE_TIMES"] = path
+    img, st = sc.render(cam, profile=True)
+    os.environ.pop("RT_WAVE_TIMES")
+a = np.fromfile(path, dtype=np.uint64).reshape(-1, 18).astype(np.float64)
+ph = a[:, 4:].sum(axis=0)
+loop = ph[7]
+out = {"scene": scene, "W": width, "spp": spp, "ms": round(st["ms_fused"], 2),
+       "segments": st["segments"], "waves": len(a)}
+for i in range(7):
+    out[NAMES[i]] = round(ph[i] / loop, 4)
+out["other"] = round(1 - (ph[0] + ph[1] + ph[2] + ph[3]) / loop, 4)
+out["trav_lane_util"] = round(ph[8] / max(ph[9], 1) / 64, 4)
+out["shade_lane_util"] = round(ph[10] / max(ph[11], 1) / 64, 4)
+out["trav_rounds_per_seg"] = round(ph[9] * 64 / max(st["segments"], 1), 3)
+out["steps_per_seg"] = round(ph[12] / max(st["segments"], 1), 2)
+out["step_simd_eff"] = round(ph[12] / max(ph[13], 1) / 64, 4)
+out["cycles_per_seg_wave"] = round(loop / max(st["segments"], 1), 1)
+print(json.dumps(out), flush=True)

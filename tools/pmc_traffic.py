@@ -33,6 +33,23 @@ PASSES = [
      "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_VMEM"],
     ["GRBM_GUI_ACTIVE", "GRBM_COUNT"],
 ]
+# PMC_SET=mem: the vector-memory path (address unit, L1, L2), for reading what binds
+# traversal; written to <tag>_pmcmem_<config>.json only (traffic.json is untouched)
+PASSES_MEM = [
+    ["TA_TA_BUSY_sum", "TA_ADDR_STALLED_BY_TC_CYCLES_sum"],
+    ["TA_DATA_STALLED_BY_TC_CYCLES_sum", "TA_FLAT_READ_WAVEFRONTS_sum"],
+    ["TCP_TOTAL_CACHE_ACCESSES_sum", "TCP_TCC_READ_REQ_sum", "TCP_TCR_TCP_STALL_CYCLES_sum",
+     "TCP_PENDING_STALL_CYCLES_sum"],
+    ["TCP_TCC_READ_REQ_LATENCY_sum", "TCP_TCP_TA_DATA_STALL_CYCLES_sum", "TCP_READ_TAGCONFLICT_STALL_CYCLES_sum"],
+    ["TCC_HIT_sum", "TCC_MISS_sum"],
+    ["TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_DRAM_sum"],
+    ["TD_TD_BUSY_sum", "TD_TC_STALL_sum", "GRBM_GUI_ACTIVE", "GRBM_COUNT"],
+    ["SQ_INSTS_VMEM", "SQ_INST_LEVEL_VMEM", "SQ_INSTS_FLAT", "SQ_WAIT_INST_LDS", "SQ_INSTS_VALU",
+     "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY"],
+]
+MEM = os.environ.get("PMC_SET") == "mem"
+if MEM:
+    PASSES = PASSES_MEM
 
 
 def run_pass(tag, counters, bench_args):
@@ -121,10 +138,13 @@ def main():
             cam.AspectRatio = 1.5
         d = cam.derived()
         key = f"{scene}:{d.width}x{d.height}x{d.spp_sqrt ** 2}"
-        raw = os.path.join(out_dir, f"{tag}_pmc_{cfg}.json")
+        raw = os.path.join(out_dir, f"{tag}_pmc{'mem' if MEM else ''}_{cfg}.json")
         with open(raw, "w") as f:
             json.dump({"config": cfg, "key": key, "bench_args": bench_args, "kernels": res}, f,
                       indent=1)
+        if MEM:
+            print(cfg, key, json.dumps(res.get("k_fused", {}).get("counters_per_launch")), flush=True)
+            continue
         db[key] = {k: {kk: v for kk, v in e.items() if kk != "counters_per_launch"}
                    for k, e in res.items()}
         for e in db[key].values():
