@@ -44,6 +44,7 @@ RT_D uint32_t fdiv(uint32_t n, const FastDiv& f) {
 struct Params {
   DevScene sc;
   FastDiv fd_npix, fd_width, fd_s;
+  FastDiv fd_gchunks, fd_gpix;  // chunk order: groups of fd_gpix.d pixels x all sample blocks
   // camera (initialize camera.go:179-253, converted to fp32)
   float p00r[3], du[3], dv[3], cc[3], dku[3], dkv[3];  // p00r = pixel00 - center
   float bg[3];
@@ -122,16 +123,26 @@ RT_D uint32_t prefix_count(unsigned long long m) {
 }
 RT_D uint32_t wave_uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// chunk c -> (local pixel, global pixel, first sample).  Chunks are pixel-fastest
-// so a wave's consecutive chunks are adjacent pixels (coherent camera rays) and
-// concurrently flushed chunks touch different accumulators.
+// chunk c -> (local pixel, global pixel, first sample).  The rank's pixels are
+// taken in groups of G = fd_gpix.d consecutive pixels (G divides npix); a group's
+// chunks are pixel-fastest over all its sample blocks, so a wave's consecutive
+// chunks are adjacent pixels (coherent camera rays, different accumulators) and the
+// chunks in flight cover only a few groups of the image (a small working set of the
+// scene for the camera rays and their first bounces) instead of the whole image.
+// G = npix is the image-wide pixel-fastest order.
 struct Ids {
   uint32_t lpix, gpix, row, col, sample0, count;
 };
+RT_D uint32_t chunk_pixel(const Params& P, uint32_t chunk, uint32_t& sub) {
+  const uint32_t q = fdiv(chunk, P.fd_gchunks);
+  const uint32_t r = chunk - q * P.fd_gchunks.d;
+  sub = fdiv(r, P.fd_gpix);
+  return q * P.fd_gpix.d + (r - sub * P.fd_gpix.d);
+}
 RT_D Ids chunk_ids(const Params& P, uint32_t chunk) {
   Ids r;
-  uint32_t sub = fdiv(chunk, P.fd_npix);
-  r.lpix = chunk - sub * P.npix;
+  uint32_t sub;
+  r.lpix = chunk_pixel(P, chunk, sub);
   uint32_t row_l = fdiv(r.lpix, P.fd_width);
   r.col = r.lpix - row_l * (uint32_t)P.width;
   r.row = row_l * (uint32_t)P.nranks + (uint32_t)P.rank;
@@ -814,7 +825,8 @@ RT_D f3 lights_random(const DevScene& sc, f3 origin, const rt_u32x4& r) {
 // (Counters::overflow, rt_stats.overflow_samples); NaN and +-Inf set pixel flags
 // with the reference's sum semantics (NaN, or +Inf and -Inf, give NaN).
 RT_D uint32_t local_pixel(const Params& P, uint32_t chunk) {
-  return chunk - fdiv(chunk, P.fd_npix) * P.npix;
+  uint32_t sub;
+  return chunk_pixel(P, chunk, sub);
 }
 // floor(v * 2^32) for |v| < 2^31: the integer part in the high word, the fraction
 // (exact: v - floor(v) loses no bits, and * 2^32 only moves the exponent) in the low

@@ -181,6 +181,9 @@ __global__ __launch_bounds__(256) void k_init(Params P) {
 #ifndef MESH_WAVES
 #define MESH_WAVES 4
 #endif
+#ifndef TRI_WAVES
+#define TRI_WAVES 4
+#endif
 #ifndef FT_TEX_WAVES
 #define FT_TEX_WAVES 4
 #endif
@@ -193,6 +196,7 @@ constexpr int fused_waves(uint32_t ft, int tree = 4) {
   return (tree == 0 && ft == 0u) ? kBruteWaves  // 7 measured within noise of 6, 8 -3 %
          : ft == 0u ? 6
          : ft == FT_MEDIA ? 4
+         : ft == (FT_SPHERE | FT_TRI | FT_METAL) ? TRI_WAVES
          : ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? MESH_WAVES
          : ft == (FT_SPHERE | FT_METAL | FT_DIEL | FT_MEDIA | FT_IMAGE | FT_NOISE) ? FT_TEX_WAVES
                                                                                   : 3;
@@ -216,7 +220,8 @@ constexpr int fused_waves(uint32_t ft, int tree = 4) {
 #define ALL_WLDS 4  // 6 pushed the C3-size trees out of the 3-wave LDS budget
 #endif
 constexpr int fused_wlds(uint32_t ft, int tree = 4) {
-  return ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? MESH_WLDS
+  return (ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ||
+          ft == (FT_SPHERE | FT_TRI | FT_METAL)) ? MESH_WLDS
          : (ft == 0u && tree != 0)                                  ? 4
          : ft == FT_ALL                                             ? ALL_WLDS
          : ft == (FT_SPHERE | FT_METAL | FT_DIEL | FT_MEDIA | FT_IMAGE | FT_NOISE) ? TEX_WLDS
@@ -748,6 +753,7 @@ static int occupancy_blocks(const void* kernel, int device, int* out, size_t dyn
 static constexpr uint32_t kFtSets[] = {
     0u,                                                     // Cornell box: quads, Lambertian, light
     FT_MEDIA,                                               // + constant media (Cornell smoke)
+    FT_SPHERE | FT_TRI | FT_METAL,                          // meshes, spheres, Lambertian + metal
     FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER,   // meshes and spheres, plain materials
     FT_SPHERE | FT_METAL | FT_DIEL | FT_MEDIA | FT_IMAGE | FT_NOISE,  // spheres, media, textures
     FT_ALL};
@@ -763,6 +769,7 @@ static const void* fused_for(uint32_t set) {
     case kFtSets[1]: return (const void*)k_fused<LDS, kFtSets[1], 4>;
     case kFtSets[2]: return (const void*)k_fused<LDS, kFtSets[2], 4>;
     case kFtSets[3]: return (const void*)k_fused<LDS, kFtSets[3], 4>;
+    case kFtSets[4]: return (const void*)k_fused<LDS, kFtSets[4], 4>;
     default: return (const void*)k_fused<LDS, FT_ALL, 4>;
   }
 }
@@ -975,6 +982,19 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   p.P = P;
   p.ss = ss;
   p.fd_npix = make_fastdiv(npix);
+  {
+    // chunk order (chunk_pixel): groups of `grows` of this rank's rows, so the paths in
+    // flight start from a band of a few rows instead of the whole image (C5 -10 %,
+    // C3 -5 %, C4 -3 %, C2 -1 % against image-wide pixel-fastest chunks; 1, 4 and 16
+    // rows measured alike, profiles/r2_chunk_order_ab.jsonl)
+    const int env_rows = env_int("RT_CHUNK_ROWS", -1);
+    uint32_t grows = env_rows > 0 ? (uint32_t)env_rows : 4u;
+    grows = std::max<uint32_t>(1u, std::min<uint32_t>(grows, std::max<uint32_t>(rows, 1u)));
+    while (rows % grows) --grows;  // a divisor of the rank's row count
+    const uint32_t gpix = std::max<uint32_t>(1u, grows * W);
+    p.fd_gpix = make_fastdiv(gpix);
+    p.fd_gchunks = make_fastdiv(gpix * cpp);
+  }
   p.fd_width = make_fastdiv(W);
   p.fd_s = make_fastdiv((uint32_t)cd.spp_sqrt);
   // Scheduling rounds, measured on the full-size configs (tools/sched_sweep.py,
