@@ -43,7 +43,7 @@ RT_D uint32_t fdiv(uint32_t n, const FastDiv& f) {
 
 struct Params {
   DevScene sc;
-  FastDiv fd_npix, fd_width, fd_s;
+  FastDiv fd_width, fd_s;
   FastDiv fd_gchunks, fd_gpix;  // chunk order: groups of fd_gpix.d pixels x all sample blocks
   // camera (initialize camera.go:179-253, converted to fp32)
   float p00r[3], du[3], dv[3], cc[3], dku[3], dkv[3];  // p00r = pixel00 - center
@@ -173,9 +173,6 @@ RT_D void camera_ray_r(const Params& P, const Ids& id, uint32_t sample, const rt
     d = d - off;
   }
   time = rt_unit_f(r.v[2]);
-}
-RT_D void camera_ray(const Params& P, const Ids& id, uint32_t sample, f3& o, f3& d, float& time) {
-  camera_ray_r(P, id, sample, rt_rng_draw(P.seed, id.gpix, sample, RT_STREAM_CAMERA), o, d, time);
 }
 
 // ------------------------------------------------------------- traversal ---
@@ -565,8 +562,10 @@ RT_D bool boundary_hit(const DevScene& sc, const DevMedium& m, f3 o, f3 d, float
 // occurrence with multiplicity m keeps the smallest of m free-flight draws.
 // Interval arithmetic in fp64: the reference searches (t1 + 1e-4, inf) with
 // |t1| up to ~1e4 (book2 fog, R = 5000), below fp32 resolution.
+// `spare`: rt_spare24 of the call that generated this ray, the scene's last draw
+// index (rt_rng.h), so the outermost medium needs no Philox call of its own.
 RT_D void trace_media(const Params& P, f3 o, f3 d, float time, float tmin, uint32_t gpix,
-                      uint32_t sample, uint32_t vertex, Hit& best) {
+                      uint32_t sample, uint32_t vertex, uint32_t spare, Hit& best) {
   const DevScene& sc = P.sc;
   rt_u32x4 r = {{0, 0, 0, 0}};
   int cached_group = -1;
@@ -595,12 +594,17 @@ RT_D void trace_media(const Params& P, f3 o, f3 d, float time, float tmin, uint3
     float hd = kInf;
     for (int k = 0; k < m.mult; ++k) {
       int draw = m.draw_base + k;
-      int group = 1 + (draw >> 2);
-      if (group != cached_group) {
-        r = rt_rng_draw(P.seed, gpix, sample, RT_STREAM(vertex, group));
-        cached_group = group;
+      float u;
+      if (draw == sc.medium_draws - 1) {
+        u = rt_unit_f(spare);
+      } else {
+        int group = 1 + (draw >> 2);
+        if (group != cached_group) {
+          r = rt_rng_draw(P.seed, gpix, sample, RT_STREAM(vertex, group));
+          cached_group = group;
+        }
+        u = rt_unit_f(r.v[draw & 3]);
       }
-      float u = rt_unit_f(r.v[draw & 3]);
       hd = fminf(hd, m.neg_inv_density * logf(u));
     }
     if ((double)hd > inside) continue;
@@ -901,6 +905,7 @@ struct Path {
   float time;
   uint32_t chunk, j, k, nst, flags;
   uint32_t gpix, s0;  // global pixel and first sample of the chunk (chunk_ids, cached)
+  uint32_t spare;     // rt_spare24 of the call that generated the ray (trace_media)
   f3 pend, pre;
   uint32_t segs;    // world.Hit calls of this lane (statistics)
   uint32_t pushes;  // clamp weights stored (statistics, RT_COUNT_PUSHES builds only)
@@ -975,7 +980,7 @@ template <bool SOA>
 RT_D void store_ray(const Params& P, uint32_t slot, const Path& s) {
   if (SOA) {
     P.ray_o[slot] = {s.o.x, s.o.y, s.o.z, s.time};
-    P.ray_d[slot] = {s.d.x, s.d.y, s.d.z, 0.0f};
+    P.ray_d[slot] = {s.d.x, s.d.y, s.d.z, bitsf(s.spare)};
     P.path[slot] = make_uint2(s.chunk, pack_path(s.j, s.k, s.nst, s.flags));
   }
 }
@@ -986,6 +991,7 @@ RT_D void load_path(const Params& P, uint32_t slot, Path& s) {
   s.o = xyz(ro);
   s.time = ro.w;
   s.d = xyz(rd);
+  s.spare = fbits(rd.w);
   s.chunk = ps.x;
   const Ids id = chunk_ids(P, s.chunk);
   s.gpix = id.gpix;
@@ -1005,6 +1011,7 @@ RT_D void next_sample(const Params& P, uint32_t slot, Path& s, uint32_t j, const
   id.row = fdiv(s.gpix, P.fd_width);
   id.col = s.gpix - id.row * (uint32_t)P.width;
   camera_ray_r(P, id, s.s0 + j, r, s.o, s.d, s.time);
+  s.spare = rt_spare24(r);
   s.j = j;
   s.k = 0;
   s.nst = 0;
@@ -1016,7 +1023,9 @@ RT_D void next_sample(const Params& P, uint32_t slot, Path& s, uint32_t j, const
 template <bool SOA>
 RT_D void start_sample(const Params& P, uint32_t slot, Path& s, uint32_t chunk, uint32_t j) {
   Ids id = chunk_ids(P, chunk);
-  camera_ray(P, id, id.sample0 + j, s.o, s.d, s.time);
+  const rt_u32x4 r = rt_rng_draw(P.seed, id.gpix, id.sample0 + j, RT_STREAM_CAMERA);
+  camera_ray_r(P, id, id.sample0 + j, r, s.o, s.d, s.time);
+  s.spare = rt_spare24(r);
   s.chunk = chunk;
   s.gpix = id.gpix;
   s.s0 = id.sample0;
@@ -1198,6 +1207,7 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
       } else {
         s.o = p;
         s.d = ndir;
+        s.spare = rt_spare24(r);
         store_ray<SOA>(P, slot, s);
         return OUT_ALIVE;
       }

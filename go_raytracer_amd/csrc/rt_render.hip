@@ -62,7 +62,7 @@ RT_D void finish_hit(const Params& P, const Path& s, Hit& best) {
 #else
   if (HAS(FT_MEDIA) && P.sc.n_media > 0)
 #endif
-    trace_media(P, s.o, s.d, s.time, 0.001f, s.gpix, s.s0 + s.j, s.k, best);
+    trace_media(P, s.o, s.d, s.time, 0.001f, s.gpix, s.s0 + s.j, s.k, s.spare, best);
   if (P.trace) record_trace(P, s, best);
 }
 
@@ -981,7 +981,6 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   p.n_chunks = n_chunks;
   p.P = P;
   p.ss = ss;
-  p.fd_npix = make_fastdiv(npix);
   {
     // chunk order (chunk_pixel): groups of `grows` of this rank's rows, so the paths in
     // flight start from a band of a few rows instead of the whole image (C5 -10 %,

@@ -22,7 +22,15 @@
  *   vertex k group 0: [0] coin (mixture pdf pdf.go:70 / dielectric materials.go:112)
  *                     [1] light pick (hittable.go:102 rand.Intn) — 24-bit integer
  *                     [2],[3] direction sample (cosine, light, sphere, fuzz)
- *   vertex k group 1+g: medium free-flight draws 4g..4g+3 (medium.go:47)
+ *   vertex k group 1+g: medium free-flight draws 4g..4g+3 (medium.go:47), except
+ *                     the scene's LAST free-flight draw index (medium_draws - 1),
+ *                     which takes the spare bits below
+ *   spare bits: every call above uses only the high 24 bits of a word, so the low
+ *   bytes of words [0],[1],[2] of the call that generated a segment's ray (the
+ *   camera group-0 call of its sample, or group 0 of the vertex that scattered it)
+ *   form one more independent 24-bit uniform, rt_spare24(); it is that segment's
+ *   last free-flight draw.  A scene whose only (or outermost, last-added) medium is
+ *   crossed by every segment (book2's fog) then needs no group-1 call at all.
  */
 #ifndef RT_RNG_H
 #define RT_RNG_H
@@ -80,6 +88,12 @@ RT_RNG_FN rt_u32x4 rt_rng_draw(uint64_t seed, uint32_t pixel, uint32_t sample, u
 }
 
 RT_RNG_FN uint32_t rt_u24(uint32_t x) { return x >> 8; }
+
+/* the 24 spare bits of a call (see the dimension map), as a word whose high 24 bits
+   hold them: rt_unit_f / rt_unit_d of it is the spare uniform */
+RT_RNG_FN uint32_t rt_spare24(rt_u32x4 r) {
+  return ((r.v[0] & 0xFFu) << 24) | ((r.v[1] & 0xFFu) << 16) | ((r.v[2] & 0xFFu) << 8);
+}
 
 RT_RNG_FN float rt_unit_f(uint32_t x) { return (float)(x >> 8) * 5.9604644775390625e-08f; }
 

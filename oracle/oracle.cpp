@@ -142,6 +142,7 @@ struct Ctx {
   uint64_t segments = 0;
   std::vector<int> med_calls;  // per medium object: calls during this world.Hit
   rt_u32x4 main{};             // group 0 of the current vertex
+  uint32_t spare = 0;          // rt_spare24 of the call that generated the current ray
   float* trace = nullptr;      // oracle_trace records
   int trace_cap = 0, trace_n = 0;
   rt_u32x4 draw(uint32_t stream) const { return rt_rng_draw(seed, gpix, sample, stream); }
@@ -602,7 +603,7 @@ struct ConstantMedium : Hittable<R> {  // medium.go:13-62
   const Hittable<R>* boundary;
   R neg_inv_density;
   const Material<R>* phase;
-  int id = 0, draw_base = 0;
+  int id = 0, draw_base = 0, spare_draw = -1;  // spare_draw: the scene's last draw index
   AABB<R> bbox() const override { return boundary->bbox(); }
   bool hit(const Ray<R>& r, Interval<R> rt, HitRecord<R>& rec, Ctx& c) const override {
     HitRecord<R> h1, h2;
@@ -616,8 +617,14 @@ struct ConstantMedium : Hittable<R> {  // medium.go:13-62
     R inside = (h2.t - h1.t) * len;
     int k = c.med_calls[id]++;
     int draw = draw_base + k;
-    rt_u32x4 q = c.draw(RT_STREAM(c.vertex, 1 + (draw >> 2)));
-    R hd = neg_inv_density * std::log(U<R>(q.v[draw & 3]));
+    uint32_t w;
+    if (draw == spare_draw) {
+      w = c.spare;  // rt_rng.h: the last draw index takes the ray's spare bits
+    } else {
+      rt_u32x4 q = c.draw(RT_STREAM(c.vertex, 1 + (draw >> 2)));
+      w = q.v[draw & 3];
+    }
+    R hd = neg_inv_density * std::log(U<R>(w));
     if (hd > inside) return false;
     rec.t = h1.t + hd / len;
     rec.p = r.at(rec.t);
@@ -887,6 +894,7 @@ struct World {
       media[i]->draw_base = base;
       base += cnt[i];
     }
+    for (auto* m : media) m->spare_draw = base - 1;
   }
 };
 
@@ -959,6 +967,7 @@ struct Renderer {
 
   Ray<R> get_ray(int i, int j, int s_i, int s_j, Ctx& c) const {  // camera.go:256-270
     rt_u32x4 r = c.draw(RT_STREAM_CAMERA);
+    c.spare = rt_spare24(r);
     R px = (((R)s_i + U<R>(r.v[0])) * recip) - R(.5);  // sampleSquareStratified :277-282
     R py = (((R)s_j + U<R>(r.v[1])) * recip) - R(.5);
     Vec3<R> ps = p00.add(du.scale((R)i + px)).add(dv.scale((R)j + py));
@@ -995,6 +1004,7 @@ struct Renderer {
     }
     if (!any) return bg;
     c.main = c.draw(RT_STREAM(c.vertex, 0));
+    c.spare = rt_spare24(c.main);  // the next segment's ray comes from this call
     Vec3<R> emit;
     if (rec.mat->emissive()) emit = rec.mat->emitted(rec);
     Scatter<R> s;
