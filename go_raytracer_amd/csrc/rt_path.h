@@ -1175,7 +1175,11 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
           float ct = dot(n, ud);
           spdf = ct < 0.0f ? 0.0f : ct * kInvPi;
         }
+#ifdef ABL_NO_LIGHTPDF
+        float pdf = 0.5f * 0.01f + 0.5f * bsdf_pdf;  // ablation build (timing only)
+#else
         float pdf = 0.5f * lights_pdf<FT>(sc, p, ndir) + 0.5f * bsdf_pdf;
+#endif
         PH_ADD(PH_LIGHT, t_light);
         weight = (att * spdf) * rcp(pdf);
         clamp_vertex = true;
@@ -1219,7 +1223,9 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
   const bool zero = lterm.x == 0.0f && lterm.y == 0.0f && lterm.z == 0.0f;
   if (!(zero && !(s.flags & F_NONFINITE))) {
     if (s.flags & F_PEND) L = clamp_contribution(get_pend<SOA>(P, slot, s) * L, P.maxc);
-    L = ws.fold(P, slot, s.nst, L);
+#ifndef ABL_NO_FOLD
+    L = ws.fold(P, slot, s.nst, L);  // (ABL_NO_FOLD: ablation build, timing only)
+#endif
     if (s.flags & F_PRE) L = get_pre<SOA>(P, slot, s) * L;
   } else {
     L = mk3(0, 0, 0);
