@@ -19,8 +19,11 @@ static uint32_t fbits_host(float f) {
 // (through checker children).  Materials and textures that are built but never
 // placed (book1's perlin orbs, main.go:52-60) do not count, so such a scene runs a
 // leaner kernel.  RT_FEATURES_ALL=1 counts every table entry (A/B).
-uint32_t scene_features(const HostScene& h) {
+// *noise_table0: every reachable noise texture uses perlin table 0, the one the
+// feature-set kernels stage in LDS (others need the all-features kernel).
+uint32_t scene_features(const HostScene& h, bool* noise_table0) {
   uint32_t f = 0;
+  if (noise_table0) *noise_table0 = true;
   std::vector<char> mat_used(h.mats.size(), 0);
   auto use_mat = [&](int m) {
     if (m >= 0 && (size_t)m < mat_used.size()) mat_used[m] = 1;
@@ -71,7 +74,10 @@ uint32_t scene_features(const HostScene& h) {
       st.push_back(T.b);
     }
     if (T.kind == RT_TEX_IMAGE) f |= FT_IMAGE;
-    if (T.kind == RT_TEX_NOISE) f |= FT_NOISE;
+    if (T.kind == RT_TEX_NOISE) {
+      f |= FT_NOISE;
+      if (T.a != 0 && noise_table0) *noise_table0 = false;
+    }
   }
   return f;
 }
@@ -89,7 +95,7 @@ int rt_scene_create(const rt_tree* t, int world, int lights, rt_scene** out) {
     delete s;
     return rc;
   }
-  s->s.h.features = rt::scene_features(s->s.h);  // walks every prim: once, not per render
+  s->s.h.features = rt::scene_features(s->s.h, &s->s.h.noise_table0);  // walks every prim: once, not per render
   *out = s;
   return RT_OK;
 }

@@ -66,6 +66,7 @@ struct HostScene {
   int32_t max_leaf = 0;
   int32_t bvh_builder = 0;  // 0 host binned SAH, 1 device PLOC
   uint32_t features = 0;    // scene_features(), computed once by rt_scene_create
+  bool noise_table0 = true; // every reachable noise texture uses perlin table 0 (scene_features)
 };
 
 struct DeviceScene;  // defined in the HIP translation unit
@@ -113,7 +114,7 @@ int build_bvh_device(HostScene& s, const std::vector<F4>& lo, const std::vector<
                      const std::vector<uint32_t>& prims, int device);
 bool bvh_device_available();
 // host_scene.cpp: RT_FT_* features a flattened scene needs
-uint32_t scene_features(const HostScene& h);
+uint32_t scene_features(const HostScene& h, bool* noise_table0 = nullptr);
 // rt_render.hip
 void release_device(Scene* s);
 

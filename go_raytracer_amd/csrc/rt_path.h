@@ -638,7 +638,12 @@ RT_D void stage_perlin(const DevScene& sc) {
   for (int i = threadIdx.x; i < (int)(sizeof(DevPerlin) / 16); i += blockDim.x) dst[i] = src[i];
 }
 
-RT_D float perlin_noise(const DevPerlin* pl, f3 p) {  // perlin.go:34-54
+// PL: const DevPerlin* (global or LDS, the all-features kernel: flat loads) or
+// LdsPerlin (table 0 in LDS, the feature-set kernels: ds_read, 3 % faster on C4
+// than flat loads and fewer spills)
+typedef __attribute__((address_space(3))) const DevPerlin* LdsPerlin;
+template <typename PL>
+RT_D float perlin_noise(PL pl, f3 p) {  // perlin.go:34-54
   float fx = floorf(p.x), fy = floorf(p.y), fz = floorf(p.z);
   float u = p.x - fx, v = p.y - fy, w = p.z - fz;
   int i = (int)fx, j = (int)fy, k = (int)fz;
@@ -650,7 +655,8 @@ RT_D float perlin_noise(const DevPerlin* pl, f3 p) {  // perlin.go:34-54
   for (int di = 0; di < 2; ++di)
     for (int dj = 0; dj < 2; ++dj)
       for (int dk = 0; dk < 2; ++dk) {
-        const F4 g = pl->ranvec[pi[di] ^ pj[dj] ^ pk[dk]];
+        const int gi = pi[di] ^ pj[dj] ^ pk[dk];
+        const F4 g = {pl->ranvec[gi].x, pl->ranvec[gi].y, pl->ranvec[gi].z, 0.0f};
         f3 wt = mk3(u - (float)di, v - (float)dj, w - (float)dk);
         accum += ((float)di * uu + (float)(1 - di) * (1 - uu)) *
                  ((float)dj * vv + (float)(1 - dj) * (1 - vv)) *
@@ -658,7 +664,8 @@ RT_D float perlin_noise(const DevPerlin* pl, f3 p) {  // perlin.go:34-54
       }
   return accum;
 }
-RT_D float perlin_turb(const DevPerlin* pl, f3 p, int depth) {  // perlin.go:57-69
+template <typename PL>
+RT_D float perlin_turb(PL pl, f3 p, int depth) {  // perlin.go:57-69
   float accum = 0.0f, weight = 1.0f;
 #pragma unroll 1  // unrolled, the scheduler hoists every octave's table reads
   for (int i = 0; i < depth; ++i) {
@@ -700,12 +707,17 @@ RT_D f3 tex_value(const DevScene& sc, int tex, float u, float v, f3 p) {
     }
     if (!HAS(FT_NOISE)) return mk3(0, 0, 0);
     // noise, texture.go:112-125 (perlin 0 from its LDS copy when staged)
-    const DevPerlin* pl = (T.a == 0 && sc.n_perlins > 0) ? &g_perlin : sc.perlins + T.a;
     const float scale = T.color.w;
     float s;
-    if (T.variant == RT_NOISE_MARBLE) s = 0.5f * (1.0f + sinf(scale * p.z + 10.0f * perlin_turb(pl, p, 7)));
-    else if (T.variant == RT_NOISE_TURBULENT) s = perlin_turb(pl, p, 7);
-    else s = 0.5f * (1.0f + perlin_noise(pl, p * scale));
+    auto eval = [&](auto pl) {
+      if (T.variant == RT_NOISE_MARBLE) return 0.5f * (1.0f + sinf(scale * p.z + 10.0f * perlin_turb(pl, p, 7)));
+      if (T.variant == RT_NOISE_TURBULENT) return perlin_turb(pl, p, 7);
+      return 0.5f * (1.0f + perlin_noise(pl, p * scale));
+    };
+    if constexpr (FT == FT_ALL)
+      s = eval((T.a == 0 && sc.n_perlins > 0) ? (const DevPerlin*)&g_perlin : sc.perlins + T.a);
+    else
+      s = eval((LdsPerlin)&g_perlin);  // table 0 (render_impl picks FT_ALL otherwise)
     return mk3(s, s, s);
   }
   return mk3(0, 0, 0);

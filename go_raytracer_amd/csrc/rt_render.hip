@@ -840,7 +840,10 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   uint32_t P;
   int fused_blocks = 0;
   const bool lds_nodes = s->h.nodes4.size() / 8 <= (size_t)kLdsNodes / 2;
-  const uint32_t feats = s->h.features, ft_set = pick_set(feats);
+  const uint32_t feats = s->h.features;
+  // the feature-set kernels read perlin table 0 from LDS only: scenes whose noise
+  // textures use other tables run the all-features kernel (generic table pointers)
+  const uint32_t ft_set = (feats & FT_NOISE) && !s->h.noise_table0 ? FT_ALL : pick_set(feats);
   // The fused kernel's LDS scene cache (stage_nodes): all BVH nodes, then the
   // leaf records when both fit, within the LDS a workgroup may take at the
   // kernel's target waves per SIMD (160 KB per CU, 24 KB of stacks per group).

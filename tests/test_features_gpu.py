@@ -29,3 +29,23 @@ def test_feature_parity(rt, oracle, gpu, name, mode):
     assert abs(st["segments"] - ost["segments"]) <= 0.01 * ost["segments"] + 10
     assert m["frac_close"] >= 0.995, m
     assert m["q_equal"] >= 0.99, m
+
+
+@pytest.mark.parametrize("tables", [1, 3])
+def test_noise_tables_kernel_choice(rt, oracle, gpu, tables):
+    """Feature-set kernels read perlin table 0 from LDS only (rt_path.h LdsPerlin); a
+    scene whose reachable noise textures use other tables runs the all-features kernel
+    (generic table pointers).  Both match the oracle."""
+    t = rt.Tree(9)
+    world, lights = scenes._room(t)
+    for i, (sc_, var) in enumerate(((0.2, rt.RT_NOISE_MARBLE), (4, rt.RT_NOISE_TURBULENT),
+                                    (4, rt.RT_NOISE_PERLIN))[:tables]):
+        t.add(world, t.sphere((-3 + 3 * i, 1, 0), 1, t.lambertian(t.noise(sc_, var))))
+    cam = scenes._cam(rt, (0, 3, -9), (0, 2, 0))
+    with rt.Scene(t, world, lights) as sc:
+        img, st = sc.render(cam, seed=5)
+    ref, _ = oracle.render(t, world, lights, cam, seed=5, threads=8)
+    assert (st["kernel_features"] == 255) == (tables > 1), st["kernel_features"]
+    m = compare(img, ref)
+    assert m["frac_close"] >= 0.995, m
+    assert m["q_equal"] >= 0.99, m
