@@ -896,15 +896,17 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     P = (uint32_t)fused_blocks * 256u;
   }
   // Samples per chunk.  Fused: the largest K in {32, 16, 8} that still gives
-  // every lane >= 48 chunks (tree in LDS) or >= 128 (tree through L1/L2, whose
-  // per-pixel cost varies more), so the last chunks do not leave most lanes idle:
-  // one GPU's share of an 8-GPU C2 runs 12 % faster at K = 8 than at 32, C5 37 %
-  // (tools/chunk_sweep.py, profiles/r1_chunk_sweep.jsonl); full one-GPU configs keep 32.
+  // every lane >= 48 chunks (tree in LDS) or >= 100 (tree through L1/L2, whose
+  // per-pixel cost varies more), so the last chunks do not leave most lanes idle.
+  // Measured with the row-group order (tools/chunk_probe.py,
+  // profiles/r2_chunk_size_*.jsonl): 8-GPU shares of C2/C3/C4/C5 are fastest at
+  // K = 8 (C5 -27 % against 32), whole images at K = 32 (C3 -3 % against 8); at 100
+  // C3 takes K = 16 (1.5 % behind 32, which is 14 % behind 8 on C5's 8-GPU share).
   uint32_t K = 32u;
   if (o.chunk > 0) {
     K = (uint32_t)o.chunk;
   } else if (mode == RT_MODE_FUSED) {
-    const uint64_t work = (uint64_t)npix * ss, need = (uint64_t)(f_lds ? 48u : 128u) * P;
+    const uint64_t work = (uint64_t)npix * ss, need = (uint64_t)(f_lds ? 48u : 100u) * P;
     K = 8u;
     for (uint32_t k : {32u, 16u})
       if (work / k >= need) {
