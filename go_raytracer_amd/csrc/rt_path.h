@@ -87,6 +87,37 @@ RT_D uint32_t pack_path(uint32_t j, uint32_t k, uint32_t nst, uint32_t flags) {
   return (j & 0xFFFu) | ((k & 0xFFu) << 12) | ((nst & 0xFFu) << 20) | ((flags & 0xFu) << 28);
 }
 
+// address-space-typed loads and stores (see trace_world's note)
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) float lds_f32;
+typedef __attribute__((address_space(1))) uint32_t glb_u32;
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4f lds_v4;
+typedef __attribute__((address_space(1))) v4f glb_v4;
+typedef float v2f __attribute__((ext_vector_type(2)));
+// 16 B from a wave-uniform address through the scalar cache (s_load into SGPRs):
+// for tables indexed by a loop counter or a broadcast index
+RT_D F4 ld_cst(const F4* p) {
+  typedef __attribute__((address_space(4))) const v4f cst_v4;
+  const v4f v = *(const cst_v4*)p;
+  return {v.x, v.y, v.z, v.w};
+}
+RT_D F4 ld_lds(const F4* p) {
+  const v4f v = *(const lds_v4*)p;
+  return {v.x, v.y, v.z, v.w};
+}
+RT_D F4 ld_glb(const F4* p) {
+  const v4f v = *(const glb_v4*)p;
+  return {v.x, v.y, v.z, v.w};
+}
+RT_D void st_lds(F4* p, F4 v) { *(lds_v4*)p = v4f{v.x, v.y, v.z, v.w}; }
+// s_waitcnt vmcnt(0) (gfx9 encoding: expcnt/lgkmcnt left unconstrained).  Placed
+// at the end of a RARE global-memory branch whose result merges with an LDS
+// branch: without it the compiler's wait lands after the merge, on the common
+// LDS path too, where it drains every outstanding store and atomic.
+RT_D void wait_vm() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+RT_D void st_glb(F4* p, F4 v) { *(glb_v4*)p = v4f{v.x, v.y, v.z, v.w}; }
+
 RT_D uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
 // Debug build (-DRT_PHASES, tools/phase_probe.py): shader-clock cycles each wave
@@ -152,23 +183,66 @@ RT_D Ids chunk_ids(const Params& P, uint32_t chunk) {
   return r;
 }
 
+// The camera constants in LDS (every kernel that starts samples stages them once,
+// stage_camera): read with broadcast ds_reads where a ray starts instead of held in
+// SGPRs for the whole kernel (the fused kernels run out of SGPRs and spill them to
+// VGPR lanes, one v_readlane per use).  [0] pixel00 - center | 1/s, [1] du | fd_s.m,
+// [2] dv | fd_s shifts, [3] center | s, [4] defocus u | defocus flag, [5] defocus v.
+__shared__ F4 g_cam[6];
+// Kernels that read the camera from g_cam: the book2 and mesh sets (C4 -3.6 %, C5 -2.3 %,
+// fewer SGPR and VGPR spills); the C2 and C3 kernels lose from it (their VGPR budget
+// takes the loaded constants: C2 +26 %), they keep them in SGPRs
+constexpr bool cam_lds(uint32_t ft) {
+  return ft == (FT_SPHERE | FT_TRI | FT_METAL) ||
+         ft == (FT_SPHERE | FT_METAL | FT_DIEL | FT_MEDIA | FT_IMAGE | FT_NOISE);
+}
+RT_D void stage_camera(const Params& P) {  // before a __syncthreads of every thread
+  if (threadIdx.x == 0) {
+    g_cam[0] = {P.p00r[0], P.p00r[1], P.p00r[2], P.recip_s};
+    g_cam[1] = {P.du[0], P.du[1], P.du[2], bitsf(P.fd_s.m)};
+    g_cam[2] = {P.dv[0], P.dv[1], P.dv[2], bitsf(P.fd_s.s1 | (P.fd_s.s2 << 8))};
+    g_cam[3] = {P.cc[0], P.cc[1], P.cc[2], bitsf((uint32_t)P.s)};
+    g_cam[4] = {P.dku[0], P.dku[1], P.dku[2], bitsf((uint32_t)P.defocus)};
+    g_cam[5] = {P.dkv[0], P.dkv[1], P.dkv[2], 0.0f};
+  }
+}
+
 // getRay camera.go:256-270 + sampleSquareStratified :277-282 + defocusDiskSample :285-290;
-// r = rt_rng_draw(seed, gpix, sample, RT_STREAM_CAMERA), drawn by the caller
+// r = rt_rng_draw(seed, gpix, sample, RT_STREAM_CAMERA), drawn by the caller.
+// CAM: the constants from g_cam (kernels that stage it, cam_lds) or from P.
+template <bool CAM>
 RT_D void camera_ray_r(const Params& P, const Ids& id, uint32_t sample, const rt_u32x4& r, f3& o,
                        f3& d, float& time) {
-  uint32_t si = fdiv(sample, P.fd_s), sj = sample - si * (uint32_t)P.s;
-  float px = (((float)sj + rt_unit_f(r.v[0])) * P.recip_s) - 0.5f;
-  float py = (((float)si + rt_unit_f(r.v[1])) * P.recip_s) - 0.5f;
+  F4 c0, c1, c2, c3;
+  FastDiv fd_s;
+  uint32_t s;
+  if (CAM) {
+    c0 = ld_lds(&g_cam[0]), c1 = ld_lds(&g_cam[1]), c2 = ld_lds(&g_cam[2]), c3 = ld_lds(&g_cam[3]);
+    const uint32_t sh = fbits(c2.w);
+    s = fbits(c3.w);
+    fd_s = {fbits(c1.w), sh & 0xFFu, sh >> 8, s};
+  } else {
+    c0 = {P.p00r[0], P.p00r[1], P.p00r[2], P.recip_s};
+    c1 = {P.du[0], P.du[1], P.du[2], 0.0f};
+    c2 = {P.dv[0], P.dv[1], P.dv[2], 0.0f};
+    c3 = {P.cc[0], P.cc[1], P.cc[2], 0.0f};
+    fd_s = P.fd_s;
+    s = (uint32_t)P.s;
+  }
+  uint32_t si = fdiv(sample, fd_s), sj = sample - si * s;
+  float px = (((float)sj + rt_unit_f(r.v[0])) * c0.w) - 0.5f;
+  float py = (((float)si + rt_unit_f(r.v[1])) * c0.w) - 0.5f;
   float fx = (float)id.col + px, fy = (float)id.row + py;
   // pixelSample - rayOrigin rearranged as (pixel00 - center) + du*fx + dv*fy - disk:
   // the same vector without fp32 cancellation against large camera coordinates
-  d = mk3(P.p00r[0] + P.du[0] * fx + P.dv[0] * fy, P.p00r[1] + P.du[1] * fx + P.dv[1] * fy,
-          P.p00r[2] + P.du[2] * fx + P.dv[2] * fy);
-  o = mk3(P.cc[0], P.cc[1], P.cc[2]);
-  if (P.defocus) {
+  d = mk3(c0.x + c1.x * fx + c2.x * fy, c0.y + c1.y * fx + c2.y * fy, c0.z + c1.z * fx + c2.z * fy);
+  o = mk3(c3.x, c3.y, c3.z);
+  if (CAM ? fbits(ld_lds(&g_cam[4]).w) != 0u : P.defocus != 0) {
+    const F4 c4 = CAM ? ld_lds(&g_cam[4]) : F4{P.dku[0], P.dku[1], P.dku[2], 0.0f};
+    const F4 c5 = CAM ? ld_lds(&g_cam[5]) : F4{P.dkv[0], P.dkv[1], P.dkv[2], 0.0f};
     rt_u32x4 q = rt_rng_draw(P.seed, id.gpix, sample, RT_STREAM_CAMERA | 1u);
     f3 dk = uniform_disk(rt_unit_f(q.v[0]), rt_unit_f(q.v[1]));
-    f3 off = mk3(P.dku[0], P.dku[1], P.dku[2]) * dk.x + mk3(P.dkv[0], P.dkv[1], P.dkv[2]) * dk.y;
+    f3 off = mk3(c4.x, c4.y, c4.z) * dk.x + mk3(c5.x, c5.y, c5.z) * dk.y;
     o = o + off;
     d = d - off;
   }
@@ -201,35 +275,6 @@ RT_D void slab(const F4& lo, const F4& hi, f3 o, f3 inv, float tmin, float tmax,
 // per thread: conflict-free ds_read/write_b32) and overflows to HBM.
 // Explicit address spaces: with generic pointers hipcc selects between the two
 // bases and emits a flat load (slower, counts against both vmcnt and lgkmcnt).
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
-typedef __attribute__((address_space(3))) float lds_f32;
-typedef __attribute__((address_space(1))) uint32_t glb_u32;
-typedef float v4f __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) v4f lds_v4;
-typedef __attribute__((address_space(1))) v4f glb_v4;
-typedef float v2f __attribute__((ext_vector_type(2)));
-// 16 B from a wave-uniform address through the scalar cache (s_load into SGPRs):
-// for tables indexed by a loop counter or a broadcast index
-RT_D F4 ld_cst(const F4* p) {
-  typedef __attribute__((address_space(4))) const v4f cst_v4;
-  const v4f v = *(const cst_v4*)p;
-  return {v.x, v.y, v.z, v.w};
-}
-RT_D F4 ld_lds(const F4* p) {
-  const v4f v = *(const lds_v4*)p;
-  return {v.x, v.y, v.z, v.w};
-}
-RT_D F4 ld_glb(const F4* p) {
-  const v4f v = *(const glb_v4*)p;
-  return {v.x, v.y, v.z, v.w};
-}
-RT_D void st_lds(F4* p, F4 v) { *(lds_v4*)p = v4f{v.x, v.y, v.z, v.w}; }
-// s_waitcnt vmcnt(0) (gfx9 encoding: expcnt/lgkmcnt left unconstrained).  Placed
-// at the end of a RARE global-memory branch whose result merges with an LDS
-// branch: without it the compiler's wait lands after the merge, on the common
-// LDS path too, where it drains every outstanding store and atomic.
-RT_D void wait_vm() { __builtin_amdgcn_s_waitcnt(0x0F70); }
-RT_D void st_glb(F4* p, F4 v) { *(glb_v4*)p = v4f{v.x, v.y, v.z, v.w}; }
 struct TravStack {
   uint32_t* lds;     // &lds_stack[0][threadIdx.x], stride blockDim.x
   uint32_t* ovf;     // &ostack[slot], stride cols
@@ -1016,13 +1061,13 @@ RT_D void load_path(const Params& P, uint32_t slot, Path& s) {
 
 // the next sample of the same chunk, its camera draw already made: the path
 // state (pixel ids cached in s) is reset for sample j
-template <bool SOA>
+template <bool SOA, bool CAM = false>
 RT_D void next_sample(const Params& P, uint32_t slot, Path& s, uint32_t j, const rt_u32x4& r) {
   Ids id;
   id.gpix = s.gpix;
   id.row = fdiv(s.gpix, P.fd_width);
   id.col = s.gpix - id.row * (uint32_t)P.width;
-  camera_ray_r(P, id, s.s0 + j, r, s.o, s.d, s.time);
+  camera_ray_r<CAM>(P, id, s.s0 + j, r, s.o, s.d, s.time);
   s.spare = rt_spare24(r);
   s.j = j;
   s.k = 0;
@@ -1032,11 +1077,11 @@ RT_D void next_sample(const Params& P, uint32_t slot, Path& s, uint32_t j, const
 }
 
 // camera ray for sample j of `chunk` (path state reset)
-template <bool SOA>
+template <bool SOA, bool CAM = false>
 RT_D void start_sample(const Params& P, uint32_t slot, Path& s, uint32_t chunk, uint32_t j) {
   Ids id = chunk_ids(P, chunk);
   const rt_u32x4 r = rt_rng_draw(P.seed, id.gpix, id.sample0 + j, RT_STREAM_CAMERA);
-  camera_ray_r(P, id, id.sample0 + j, r, s.o, s.d, s.time);
+  camera_ray_r<CAM>(P, id, id.sample0 + j, r, s.o, s.d, s.time);
   s.spare = rt_spare24(r);
   s.chunk = chunk;
   s.gpix = id.gpix;
@@ -1247,7 +1292,7 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
   if (s.j + 1 < count) {
     if (!have_rcam)  // a miss, or the depth limit: the camera draw is made here
       rcam = rt_rng_draw(P.seed, s.gpix, s.s0 + s.j + 1, RT_STREAM_CAMERA);
-    next_sample<SOA>(P, slot, s, s.j + 1, rcam);
+    next_sample<SOA, cam_lds(FT)>(P, slot, s, s.j + 1, rcam);
     PH_ADD(PH_TERM, t_term);
     return OUT_ALIVE;
   }

@@ -35,3 +35,17 @@ with rt.Scene(t, w, l) as sc:
             "idle_frac": round(float(np.sum(span - end) / (span * len(a))), 4),
             "segments_p50": q(a[:, 2], 50), "segments_min": int(a[:, 2].min()),
             "segments_max": int(a[:, 2].max())}), flush=True)
+        # end times by XCD (workgroups are dispatched round-robin: block % 8) and by the
+        # wave's slot in its workgroup (one workgroup per CU slot: its 4 waves, one per SIMD)
+        blk = np.arange(len(a)) // 4
+        xcd = {int(x): round(float(np.percentile(end[blk % 8 == x], 50)), 1) for x in range(8)}
+        xcd_max = {int(x): round(float(end[blk % 8 == x].max()), 1) for x in range(8)}
+        nblk = len(a) // 4
+        resident = nblk // 256  # workgroups per CU
+        by_slot = {int(r): round(float(np.percentile(end[(blk // 256) % max(resident, 1) == r], 50)), 1)
+                   for r in range(max(resident, 1))}
+        seg_slot = {int(r): int(np.median(a[(blk // 256) % max(resident, 1) == r, 2]))
+                    for r in range(max(resident, 1))}
+        print(json.dumps({"nranks": n, "end_p50_by_xcd_us": xcd, "end_max_by_xcd_us": xcd_max,
+                          "end_p50_by_dispatch_round_us": by_slot,
+                          "segments_p50_by_dispatch_round": seg_slot}), flush=True)
