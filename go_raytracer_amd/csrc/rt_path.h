@@ -735,6 +735,12 @@ RT_D f3 tex_value(const DevScene& sc, int tex, float u, float v, f3 p) {
       tex = ((x + y + z) % 2 == 0) ? T.a : T.b;
       continue;
     }
+#ifdef ABL_NO_IMAGE
+    if (HAS(FT_IMAGE) && T.kind == RT_TEX_IMAGE) return xyz(T.color);  // ablation build (timing only)
+#endif
+#ifdef ABL_NO_NOISE
+    if (HAS(FT_NOISE) && T.kind == RT_TEX_NOISE) return xyz(T.color);  // ablation build (timing only)
+#endif
     if (HAS(FT_IMAGE) && (!HAS(FT_NOISE) || T.kind == RT_TEX_IMAGE)) {  // texture.go:70-86 + PixelData imageLoader.go:52-62
       const DevImage im = sc.images[T.a];
       if (im.h <= 0) return mk3(0, 1, 1);
