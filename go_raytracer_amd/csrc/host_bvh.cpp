@@ -69,11 +69,12 @@ static double env_d(const char* n, double d) {
 int build_bvh(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi,
               const std::vector<uint32_t>& prims) {
   const int n = (int)prims.size();
-  // SAH may stop at <= kLeafTarget prims.  Measured (tools/bvh_sweep.sh, profiles/):
-  // small scenes, whose leaves sit in LDS, are fastest with leaves of up to 4;
-  // large ones (C4 3.4k prims, C5 1M) are 11 % faster with single-prim leaves,
-  // the parent's child box culling each prim before its record is fetched.
-  const int kLeafTarget = std::min(env_i("RT_BVH_LEAF", n > 1024 ? 1 : 4), MAX_LEAF);
+  // SAH may stop at <= kLeafTarget prims.  Measured (tools/bvh_sweep.sh, tools/leaf_ab.sh,
+  // profiles/): small scenes, whose tree and leaves sit in LDS, are fastest with leaves
+  // of up to 4; trees read through L1/L2 (C3 485 prims, C4 3.4k, C5 1M) with single-prim
+  // leaves (C4/C5 -11 %, C3 -1.6 %), the parent's child box culling each prim before its
+  // record is fetched.  Above 256 prims a tree no longer fits the LDS cache.
+  const int kLeafTarget = std::min(env_i("RT_BVH_LEAF", n > 256 ? 1 : 4), MAX_LEAF);
   const double kCostTrav = env_d("RT_BVH_CT", 1.0), kCostIsect = env_d("RT_BVH_CI", 1.0);
   s.nodes.clear();
   s.refs.clear();

@@ -10,7 +10,7 @@ cam.Width, cam.SamplesPerPixel = width, spp
 if scene == "book1": cam.AspectRatio = 1.5
 with rt.Scene(t, w, l) as sc:
     sc.render(cam, nranks=n)
-    for k in (8, 16, 32):
+    for k in [int(x) for x in os.environ.get("KS", "8,16,32").split(",")]:
         ms = []
         for _ in range(2):
             _, st = sc.render(cam, nranks=n, chunk=k, profile=True)
