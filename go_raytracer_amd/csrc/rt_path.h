@@ -1019,8 +1019,37 @@ struct WStack {
     return (size_t)(k - nlds) * P.P + slot;
 #endif
   }
-  // backward clamp fold over entries nst-1 .. 0 (camera.go:328-330): the HBM
-  // entries (rare) one by one, the LDS entries read together and applied unrolled
+  // The backward clamp fold (camera.go:328-330) as one scale.  A clamp only scales its
+  // vector, by s_k = min(1, M / I(w_k (.) v_k+1)) with I the channel sum, so the folded
+  // value is (prod s_k) times the plain product P_0 = w_0 (.) ... (.) w_n (.) L, and the
+  // scales telescope: prod s_k = min(1, min_k M / I(P_k)) over the suffix products
+  // P_k = w_k (.) ... (.) L.  So the walk from the last weight back multiplies and
+  // keeps the largest channel sum; one scale by M / max I at the end (if max I > M)
+  // replaces a compare, reciprocal and select per clamp vertex.  Same value as the
+  // step-by-step clamps up to fp32 rounding (weights and radiance are non-negative).
+  // `v` is pend (.) L with maxI = I(v) on entry; entries nst-1 .. 0: HBM ones (rare)
+  // one by one, then the LDS ones, unrolled.
+  RT_D void fold_max(const Params& P, uint32_t slot, uint32_t nst, f3& v, float& maxI) const {
+    for (int k = (int)nst - 1; k >= nlds; --k) {
+      v = xyz(ld_glb(P.stack + hbm_index(P, slot, (uint32_t)k))) * v;
+      maxI = fmaxf(maxI, v.x + v.y + v.z);
+    }
+    if (nlds > 0 && nst > 0) {
+      const lds_f32* q = (const lds_f32*)lds;
+      f3 e[kLdsWMax];
+#pragma unroll
+      for (int i = 0; i < kLdsWMax; ++i)
+        if (i < nlds)  // entries >= nst are garbage, unused
+          e[i] = mk3(q[i * 256], q[(nlds + i) * 256], q[(2 * nlds + i) * 256]);
+#pragma unroll
+      for (int i = kLdsWMax - 1; i >= 0; --i)
+        if (i < nlds && i < (int)nst) {
+          v = e[i] * v;
+          maxI = fmaxf(maxI, v.x + v.y + v.z);
+        }
+    }
+  }
+  // the step-by-step fold (A/B builds: -DRT_FOLD_STEPWISE)
   RT_D f3 fold(const Params& P, uint32_t slot, uint32_t nst, f3 L) const {
     for (int k = (int)nst - 1; k >= nlds; --k)
       L = clamp_contribution(xyz(ld_glb(P.stack + hbm_index(P, slot, (uint32_t)k))) * L, P.maxc);
@@ -1285,9 +1314,17 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
   f3 L = lterm;
   const bool zero = lterm.x == 0.0f && lterm.y == 0.0f && lterm.z == 0.0f;
   if (!(zero && !(s.flags & F_NONFINITE))) {
+#ifdef RT_FOLD_STEPWISE
     if (s.flags & F_PEND) L = clamp_contribution(get_pend<SOA>(P, slot, s) * L, P.maxc);
-#ifndef ABL_NO_FOLD
-    L = ws.fold(P, slot, s.nst, L);  // (ABL_NO_FOLD: ablation build, timing only)
+    L = ws.fold(P, slot, s.nst, L);
+#elif !defined(ABL_NO_FOLD)  // (ABL_NO_FOLD: ablation build, timing only)
+    float maxI = 0.0f;  // no clamp vertex: no scale
+    if (s.flags & F_PEND) {
+      L = get_pend<SOA>(P, slot, s) * L;
+      maxI = L.x + L.y + L.z;
+      ws.fold_max(P, slot, s.nst, L, maxI);
+    }
+    if (maxI > P.maxc) L = L * (P.maxc * rcp(maxI));
 #endif
     if (s.flags & F_PRE) L = get_pre<SOA>(P, slot, s) * L;
   } else {
