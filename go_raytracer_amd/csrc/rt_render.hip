@@ -1004,12 +1004,16 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   p.fd_width = make_fastdiv(W);
   p.fd_s = make_fastdiv((uint32_t)cd.spp_sqrt);
   // Scheduling rounds, measured on the full-size configs (tools/sched_sweep.py,
-  // profiles/r1_sched_sweep*.jsonl): trees read through L1/L2 gain from bounded
-  // rounds of 8 steps (C5 +75 %, C4 +10 %) so short rays do not idle behind long
-  // ones; LDS-resident trees (C2, C3) lose from any bound.  The all-features
-  // kernel, whose shading is long, also gains from shading 32+ lanes at once.
-  p.step_budget = env_int("RT_STEP_BUDGET", f_lds ? (1 << 30) : 8);
-  p.shade_min = (uint32_t)env_int("RT_SHADE_MIN", !f_lds && ft_set == FT_ALL ? 32 : 1);
+  // tools/sched_ab.sh, profiles/r1_sched_sweep*.jsonl, r2_sched_ab*.jsonl): trees read
+  // through L1/L2 gain from bounded rounds so short rays do not idle behind long ones —
+  // 8 steps for large trees (C5 +75 %, C4 +10 % over unbounded), 12 for small ones
+  // (C3's 485 spheres: 7 % faster than 8); LDS-resident trees (C2) lose from any bound.
+  // Kernels with long shading gain from waiting until enough lanes are ready: 32 for
+  // the book2 and all-features sets (C4 -1.2 %), 16 for large trees otherwise (C5 -2 %).
+  const bool big_tree = s->h.nodes4.size() / 8 >= 1024;
+  p.step_budget = env_int("RT_STEP_BUDGET", f_lds ? (1 << 30) : big_tree ? 8 : 12);
+  const bool long_shade = ft_set == FT_ALL || (ft_set & FT_NOISE);
+  p.shade_min = (uint32_t)env_int("RT_SHADE_MIN", f_lds ? 1 : long_shade ? 32 : big_tree ? 16 : 1);
   // chunks per refill of a wave's batch (one returning atomic on the chunk
   // counter each): C2 grab sweep (profiles/r1_grab_sweep.jsonl) 64 -> 128:
   // -4 % at 1-2 ranks' shares; 256 for small chunks: -11 % on the 8-GPU share
