@@ -208,7 +208,7 @@ constexpr int fused_waves(uint32_t ft, int tree = 4) {
 #define MESH_WLDS 4
 #endif
 #ifndef MESH_SHORT
-#define MESH_SHORT kShortStack
+#define MESH_SHORT 16  // C5's 1M-triangle tree: -1.3 % against 12 (r2_mesh_short_ab.jsonl)
 #endif
 #ifndef TEX_SHORT
 #define TEX_SHORT kShortStack
@@ -232,7 +232,8 @@ constexpr int fused_wlds(uint32_t ft, int tree = 4) {
 constexpr int fused_short(uint32_t ft, int tree = 4) {
   return tree == 0                                                    ? 0
          : ft == 0u                                                   ? kShortStackMin
-         : ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? MESH_SHORT
+         : (ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ||
+            ft == (FT_SPHERE | FT_TRI | FT_METAL)) ? MESH_SHORT
          : ft == (FT_SPHERE | FT_METAL | FT_DIEL | FT_MEDIA | FT_IMAGE | FT_NOISE) ? TEX_SHORT
                                                                       : kShortStack;
 }
