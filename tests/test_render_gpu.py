@@ -209,3 +209,21 @@ def test_maxcontribution_clamp_on_gpu(rt, gpu):
         s = img.astype(np.float64).sum(axis=2)
         assert (s <= maxc * (1 + 1e-5)).all(), (maxc, s.max())
         assert (np.abs(s - maxc) < 1e-4 * maxc).mean() > 0.05
+
+
+@pytest.mark.parametrize("name", ["book2", "book1"])
+def test_image_independent_of_schedule_knobs(rt, gpu, name, monkeypatch):
+    """The chunk order (row groups), the traversal step budget, the ready-lane count
+    before shading and the chunk batch size only change WHEN work runs, never what a
+    sample computes: with exact pixel sums the image is bit-identical under every
+    setting (rt_render.hip RT_CHUNK_ROWS / RT_STEP_BUDGET / RT_SHADE_MIN / RT_GRAB_MIN)."""
+    t, cam, w, l = _scene(rt, name, 64, 64)
+    with rt.Scene(t, w, l) as sc:
+        base, _ = sc.render(cam, seed=6)
+        for var, val in (("RT_CHUNK_ROWS", "1"), ("RT_CHUNK_ROWS", "100000"),
+                         ("RT_STEP_BUDGET", "3"), ("RT_STEP_BUDGET", "1000000"),
+                         ("RT_SHADE_MIN", "40"), ("RT_GRAB_MIN", "1")):
+            monkeypatch.setenv(var, val)
+            img, _ = sc.render(cam, seed=6)
+            monkeypatch.delenv(var)
+            assert np.array_equal(base, img, equal_nan=True), (var, val)
