@@ -138,6 +138,10 @@ struct DevScene {
   const DevPerlin* perlins;
   int32_t brute_ax[3];  // record loop (TREE 0): axis-aligned pairs per normal axis, after
                         // the general pairs (host-grouped; rt_path.h brute_axis)
+  int32_t brute_vt[3];  // record loop: pairs parallel to an axis (n_a = A_a = 0, B along a:
+                        // the sides of boxes rotated about a), between the general and the
+                        // axis-aligned pairs (rt_path.h brute_vert; only y is grouped: RotateY
+                        // is the reference's only rotation, transformation.go:48)
   int32_t n_perlins;    // perlin 0's tables are staged in LDS by the noise kernels
 };
 

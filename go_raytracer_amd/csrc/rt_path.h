@@ -515,12 +515,45 @@ RT_D void brute_axis(const DevScene& sc, const F4* lrec, int p0, int p1, const v
     bk = c1 ? k1 : bk;
   }
 }
+// Pairs parallel to axis AX (host-grouped): n_AX = 0 and A_AX = 0 exactly and B has only
+// its AX component (NewBox's side faces after RotateY: v is the vertical edge).  Each
+// dropped term of the general test is an exact zero, so den, num, alpha and beta are the
+// general test's values (up to the sign of an exact zero): 15 packed ops per pair instead
+// of 20.  (r: n.x 0, n.y 1, n.z 2 | Q 2-3 | A 3-4 | B 5-6, as pair_q/a/b)
+template <int I> RT_D v2f pair_n(const v4f* r) { return I == 0 ? r[0].xy : I == 1 ? r[0].zw : r[1].xy; }
+template <int AX, bool SMEM>
+RT_D void brute_vert(const DevScene& sc, const F4* lrec, int p0, int p1, const v2f* O,
+                     const v2f* Dv, float tmin, float& best, uint32_t& bk) {
+  constexpr int B0 = AX == 0 ? 1 : 0, B1 = AX == 2 ? 1 : 2;  // the other axes, ascending
+  for (int p = p0; p < p1; ++p) {
+    v4f r[7];
+    load_pair<SMEM>(sc, lrec, p, r);
+    const uint32_t k0 = __float_as_uint(r[6].z), k1 = __float_as_uint(r[6].w);
+    const v2f D = r[1].zw;
+    const v2f den = pfma(pair_n<B1>(r), Dv[B1], pair_n<B0>(r) * Dv[B0]);
+    const v2f num = D - pfma(pair_n<B1>(r), O[B1], pair_n<B0>(r) * O[B0]);
+    const v2f t = num * v2f{rcp(den.x), rcp(den.y)};
+    const v2f pa = pfma(Dv[AX], t, O[AX]) - pair_q<AX>(r);
+    const v2f p0v = pfma(Dv[B0], t, O[B0]) - pair_q<B0>(r);
+    const v2f p1v = pfma(Dv[B1], t, O[B1]) - pair_q<B1>(r);
+    const v2f a = pfma(p1v, pair_a<B1>(r), p0v * pair_a<B0>(r));
+    const v2f b = pa * pair_b<AX>(r);
+    const bool c0 = fabsf(den.x) >= 1e-8f && t.x >= tmin && unit_ab(a.x, b.x) && t.x <= best;
+    best = c0 ? t.x : best;
+    bk = c0 ? k0 : bk;
+    const bool c1 = fabsf(den.y) >= 1e-8f && t.y >= tmin && unit_ab(a.y, b.y) && t.y <= best;
+    best = c1 ? t.y : best;
+    bk = c1 ? k1 : bk;
+  }
+}
 template <uint32_t FT, bool SMEM>
 RT_D void trav_brute(const DevScene& sc, const F4* lrec, f3 o, f3 d, float time, float tmin,
                      Trav& tr) {
   static_assert(!HAS(FT_SPHERE | FT_TRI), "record loop: quad-only feature sets");
   const int nax = sc.brute_ax[0], nay = sc.brute_ax[1], naz = sc.brute_ax[2];
-  const int ng = (sc.n_refs >> 1) - nax - nay - naz;  // general pairs first (even count)
+  const int nvy = sc.brute_vt[1];  // y-parallel pairs only (RotateY is the only rotation)
+  // general pairs first, then the y-parallel and the axis-aligned groups
+  const int ng = (sc.n_refs >> 1) - nax - nay - naz - nvy;
   const v2f ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
   const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z};
   float best = tr.best.t;
@@ -548,9 +581,11 @@ RT_D void trav_brute(const DevScene& sc, const F4* lrec, f3 o, f3 d, float time,
     bk = c1 ? k1 : bk;
   }
   const v2f O[3] = {ox, oy, oz}, Dv[3] = {dx, dy, dz};
-  brute_axis<0, SMEM>(sc, lrec, ng, ng + nax, O, Dv, tmin, best, bk);
-  brute_axis<1, SMEM>(sc, lrec, ng + nax, ng + nax + nay, O, Dv, tmin, best, bk);
-  brute_axis<2, SMEM>(sc, lrec, ng + nax + nay, ng + nax + nay + naz, O, Dv, tmin, best, bk);
+  const int q = ng + nvy;
+  brute_vert<1, SMEM>(sc, lrec, ng, q, O, Dv, tmin, best, bk);
+  brute_axis<0, SMEM>(sc, lrec, q, q + nax, O, Dv, tmin, best, bk);
+  brute_axis<1, SMEM>(sc, lrec, q + nax, q + nax + nay, O, Dv, tmin, best, bk);
+  brute_axis<2, SMEM>(sc, lrec, q + nax + nay, q + nax + nay + naz, O, Dv, tmin, best, bk);
   if (bk != 0xFFFFFFFFu) {
     // the winner's fields (pair bk/2, half bk&1): Q at floats 8/10/12, A at
     // 14/16/18, B at 20/22/24, ref at 28 (+ half)

@@ -641,12 +641,26 @@ static int upload_scene(const Scene* s, DeviceScene* ds) {
       }
       return -1;
     };
-    std::vector<size_t> grp[4];  // 0-2: axis groups, 3: general
+    // y-parallel quads (n_y = A_y = 0 and B = (0, B_y, 0) exactly: the sides of Cornell's
+    // boxes rotated about y) go in a pair group between the general and the axis-aligned
+    // ones (rt_path.h brute_vert: the general test without its exact-zero terms, images
+    // bit-identical; C2 -1.6 % against RT_BRUTE_VERT=0, which keeps them general).
+    const bool use_vert = env_int("RT_BRUTE_VERT", 1) != 0;
+    auto vert_of = [&](size_t i) -> int {
+      const F4* r = &recs[4 * i];
+      if (!use_vert || (h.refs[i] >> 30) != PRIM_QUAD || axis_of(i) >= 0) return -1;
+      const float n[3] = {r[1].x, r[1].y, r[1].z}, A[3] = {r[2].x, r[2].y, r[2].z},
+                  B[3] = {r[3].x, r[3].y, r[3].z};
+      // y only (brute_vert<1>): RotateY is the reference's only rotation
+      return n[1] == 0.0f && A[1] == 0.0f && B[0] == 0.0f && B[2] == 0.0f && B[1] != 0.0f ? 1 : -1;
+    };
+    std::vector<size_t> grp[7];  // 0-2: axis-aligned groups, 3: general, 4-6: axis-parallel
     for (size_t i : ord) {
       const int a = axis_of(i);
-      grp[a < 0 ? 3 : a].push_back(i);
+      const int v = a < 0 ? vert_of(i) : -1;
+      grp[a >= 0 ? a : v >= 0 ? 4 + v : 3].push_back(i);
     }
-    for (int a = 0; a < 3; ++a)
+    for (int a : {0, 1, 2, 4, 5, 6})
       if (grp[a].size() & 1) {
         grp[3].push_back(grp[a].back());  // the group's smallest record
         grp[a].pop_back();
@@ -656,7 +670,11 @@ static int upload_scene(const Scene* s, DeviceScene* ds) {
     std::vector<long> slots;  // record per slot in loop order, -1 = pad
     for (size_t i : grp[3]) slots.push_back((long)i);
     if (slots.size() & 1) slots.push_back(-1);
-    const size_t n_general = slots.size();
+    for (int a = 0; a < 3; ++a) {
+      for (size_t i : grp[4 + a]) slots.push_back((long)i);
+      d.brute_vt[a] = (int32_t)(grp[4 + a].size() / 2);
+    }
+    const size_t n_general = slots.size();  // general and axis-parallel: the stored D
     for (int a = 0; a < 3; ++a) {
       for (size_t i : grp[a]) slots.push_back((long)i);
       d.brute_ax[a] = (int32_t)(grp[a].size() / 2);
