@@ -136,20 +136,23 @@ def test_kernel_selection(rt, gpu, name, width, lean, width_tree, lds):
         assert st["lds_scene"] == lds
 
 
-def test_axis_record_groups_match_general_test(rt, gpu, monkeypatch):
-    """The record loop's axis-aligned groups (rt_path.h brute_axis) compute the
-    general quad test's t, alpha and beta bit for bit: the Cornell box renders the
-    same image with the grouping switched off (RT_BRUTE_AXIS=0)."""
-    t, cam, w, l = rt.demo_scene("cornell")
+@pytest.mark.parametrize("var", ["RT_BRUTE_AXIS", "RT_BRUTE_VERT"])
+@pytest.mark.parametrize("name", ["cornell", "cornell_smoke"])
+def test_axis_record_groups_match_general_test(rt, gpu, monkeypatch, var, name):
+    """The record loop's axis-aligned groups (rt_path.h brute_axis) and its y-parallel
+    group (brute_vert: the rotated boxes' sides) compute the general quad test's t,
+    alpha and beta bit for bit: the Cornell boxes render the same image with either
+    grouping switched off (RT_BRUTE_AXIS=0 / RT_BRUTE_VERT=0)."""
+    t, cam, w, l = rt.demo_scene(name)
     cam.Width, cam.SamplesPerPixel = 96, 64
     imgs = []
     for flag in ("0", "1"):
-        monkeypatch.setenv("RT_BRUTE_AXIS", flag)
+        monkeypatch.setenv(var, flag)
         with rt.Scene(t, w, l) as sc:
             img, st = sc.render(cam, seed=4)
         assert st["tree_width"] == 0
         imgs.append(img)
-    assert np.array_equal(imgs[0], imgs[1])
+    assert np.array_equal(imgs[0], imgs[1], equal_nan=True)
 
 
 def test_render_multi_same_device_is_bitwise(rt, gpu):
