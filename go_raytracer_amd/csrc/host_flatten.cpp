@@ -519,7 +519,7 @@ int flatten_scene(const Tree& t, int world, int lights, HostScene& out) {
   if (builder == "device" && !on_device && f.world_refs.size() >= 2)
     return set_error(RT_ERR_DEVICE, "RT_BVH_BUILDER=device but no HIP device is available");
   out.bvh_builder = on_device ? 1 : 0;
-  rc = on_device ? build_bvh_device(out, f.lo, f.hi, f.world_refs, 0)
+  rc = on_device ? build_bvh_device(out, f.lo, f.hi, f.world_refs, -1)  // current device
                  : build_bvh(out, f.lo, f.hi, f.world_refs);
   if (timing)
     fprintf(stderr, "[rt] build_bvh (%s) %.3f s\n", on_device ? "device" : "host",

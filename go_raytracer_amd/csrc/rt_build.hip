@@ -441,6 +441,15 @@ int build_bvh_device(HostScene& s, const std::vector<F4>& lo, const std::vector<
   if ((uint32_t)n > 0x7FFFFFFu) return set_error(RT_ERR_UNSUPPORTED, "too many prims (%d)", n);
   const bool timing = getenv("RT_TIMING") != nullptr;
   auto t0 = std::chrono::steady_clock::now();
+  // device < 0: the calling thread's current device (one process per GPU builds on its
+  // own GPU); the caller's current device is restored on return
+  int prev = 0;
+  B_OK(hipGetDevice(&prev));
+  if (device < 0) device = prev;
+  struct DeviceGuard {
+    int d;
+    ~DeviceGuard() { (void)hipSetDevice(d); }
+  } dg{prev};
   B_OK(hipSetDevice(device));
   hipStream_t st;
   B_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));

@@ -109,7 +109,8 @@ int flatten_scene(const Tree& t, int world, int lights, HostScene& out);
 // host_bvh.cpp
 int build_bvh(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi,
               const std::vector<uint32_t>& prims);
-// rt_build.hip: the same outputs as build_bvh, built by PLOC on `device`
+// rt_build.hip: the same outputs as build_bvh, built by PLOC on `device` (-1: the calling
+// thread's current device; the current device is restored on return)
 int build_bvh_device(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi,
                      const std::vector<uint32_t>& prims, int device);
 bool bvh_device_available();

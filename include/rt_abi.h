@@ -267,7 +267,8 @@ typedef struct rt_scene rt_scene;
 
 /* Flatten world/lights (transforms baked, media separated, light table built)
  * and build the device BVH (BuildBVH bvh.go:21-61 + the world list).  Scenes of
- * >= 65536 world prims build it on HIP device 0 (PLOC, DESIGN.md "BVH") when one is
+ * >= 65536 world prims build it on the calling thread's current HIP device (PLOC,
+ * DESIGN.md "BVH"; the current device is left unchanged) when one is
  * present, otherwise with the host binned-SAH builder; RT_BVH_BUILDER=host|device
  * overrides, RT_BVH_DEVICE_MIN moves the threshold.  lights may be -1. */
 int rt_scene_create(const rt_tree* t, int world, int lights, rt_scene** out);
