@@ -65,6 +65,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra-configs", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline work")
+    ap.add_argument("--devices", default=None,
+                    help="single-process multi-GPU: comma-separated HIP devices rendered through "
+                         "rt_render_multi (rows r on devices[r %% n], peer-gathered to devices[0]); "
+                         "the north_star's Go-host path, no torchrun")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"),
                     help="PMC counters per launch (tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -141,13 +145,20 @@ def load_traffic(path):
         return {}
 
 
-def roofline(db, key, kernel, ms, seg, smp, pix):
-    """Rooflines of one launch of `kernel` (ms = live average launch time)."""
+def roofline(db, key, kernel, ms, seg, smp, pix, full_smp):
+    """Rooflines of one launch of `kernel` (ms = live average launch time).  The PMC
+    counts are per launch over the whole image (tools/pmc_traffic.py, one GPU); a launch
+    that renders a row share (multi-GPU) is charged its share of them, smp / full_smp."""
     model_bytes = seg * B_PER_SEG + smp * B_PER_SAMPLE + pix * B_PER_PIXEL
     model_gbs = model_bytes / max(ms, 1e-9) / 1e6
     pmc = db.get(key, {}).get(kernel, {})
+    share = smp / full_smp if full_smp else 1.0
     valu = pmc.get("valu_insts_per_launch")
     hbm = pmc.get("hbm_bytes_per_launch")
+    if valu:
+        valu *= share
+    if hbm:
+        hbm *= share
     r = {"bound": "issue", "kernel": kernel, "achieved": None, "peak": PEAK_VALU_GIPS,
          "unit": "G VALU wave-instr/s", "frac": None, "traffic": hbm}
     if valu:
@@ -167,6 +178,8 @@ def roofline(db, key, kernel, ms, seg, smp, pix):
                                "in registers/LDS and does not move these bytes)"}
     if pmc.get("_source"):
         r["pmc_source"] = pmc["_source"]
+    if share < 0.999:
+        r["pmc_share"] = round(share, 6)
     return r
 
 
@@ -180,10 +193,19 @@ def main():
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world_size != args.gpus and not (world_size == 1 and args.gpus == 1):
+    devices = [int(x) for x in args.devices.split(",")] if args.devices else None
+    if devices:
+        if world_size != 1:
+            raise SystemExit("--devices is the single-process mode: do not launch it with torchrun")
+        if len(devices) != args.gpus:
+            raise SystemExit("--devices must list --gpus devices")
+        local_rank = devices[0]
+    elif world_size != args.gpus and not (world_size == 1 and args.gpus == 1):
         if world_size == 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run "
+                             "(or use --devices for one process over N GPUs)")
     torch.cuda.set_device(local_rank)
+    nshare = len(devices) if devices else 1  # row shares per launch statistic
     dev = torch.device("cuda", local_rank)
     if world_size > 1:
         dist.init_process_group("nccl", device_id=dev)
@@ -194,6 +216,9 @@ def main():
         """warmup + `steps` renders of this rank's share (+ all_gather), barrier and
         synchronize around the timed region; returns (max elapsed, per-step stats)."""
         def step(prof):
+            if devices:  # one process: every share on its device, gathered on devices[0]
+                return scene.render_multi_device(cam, devices, buf.data_ptr(), seed=args.seed,
+                                                 profile=prof, mode=args.mode)
             st = scene.render_device(cam, buf.data_ptr(), seed=args.seed, device=local_rank,
                                      rank=rank, nranks=world_size, profile=prof,
                                      stream=stream.cuda_stream, mode=args.mode)
@@ -223,6 +248,8 @@ def main():
         return t.item(), stats, t_first
 
     def buffers(d):
+        if devices:  # the whole image on devices[0]
+            return torch.zeros((d.height, d.width, 3), dtype=torch.float32, device=dev), None
         rows_per = (d.height + world_size - 1) // world_size
         buf = torch.zeros((rows_per, d.width, 3), dtype=torch.float32, device=dev)
         gathered = torch.zeros((world_size * rows_per, d.width, 3), dtype=torch.float32,
@@ -255,8 +282,9 @@ def main():
         key = f"{args.scene}:{W}x{H}x{d.spp_sqrt ** 2}"
         if mode == "fused":
             ms = sum(s["ms_fused"] for s in stats) / len(stats)
-            roof = roofline(db, key, "k_fused", ms, seg / len(stats), smp / len(stats),
-                            pix / len(stats))
+            k = len(stats) * nshare  # per device launch (the slowest share's time)
+            roof = roofline(db, key, "k_fused", ms, seg / k, smp / k, pix / k,
+                            W * H * d.spp_sqrt ** 2)
             roof["launches"] = len(stats)
             roof["avg_ms"] = round(ms, 4)
         else:  # the wavefront pair: the model's bytes per kernel (cross-check path)
@@ -275,18 +303,21 @@ def main():
         t_ppm0 = time.perf_counter()
         ppm = rt.format_ppm_device(buf if world_size == 1 else
                                    shard.assemble(gathered, H, world_size))
+        n_gpus = len(set(devices)) if devices else world_size
         t_ppm = time.perf_counter() - t_ppm0
         value = total_samples / elapsed / 1e6
         line = {
             "metric": "Msamples/sec (pixels×spp/s) + wall-clock, Cornell Box 800×800×1024spp",
-            "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world_size,
+            "value": round(value, 3), "unit": "Msamples/s", "n_gpus": n_gpus,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": f"{args.scene} {W}x{H} {d.spp_sqrt ** 2}spp maxdepth "
                                    f"{d.max_depth} (BASELINE configs[1], main.go cornellBox)",
                        "scene": args.scene, "width": W, "height": H, "spp": d.spp_sqrt ** 2,
-                       "max_depth": d.max_depth, "parallelism": f"rows%{world_size}",
+                       "max_depth": d.max_depth,
+                       "parallelism": (f"rows%{len(devices)} in one process (rt_render_multi, "
+                                       f"devices {devices})") if devices else f"rows%{world_size}",
                        "mode": mode, "path_slots": stats[0]["path_slots"],
                        "chunk_samples": stats[0]["chunk_samples"],
                        "segments_per_sample": round(seg / max(smp, 1), 4),
@@ -339,12 +370,13 @@ def main():
             if world_size > 1:
                 dist.all_reduce(tot, op=dist.ReduceOp.SUM)
             if rank == 0:
-                seg = sum(s["segments"] for s in st2) / steps
-                smp = sum(s["samples"] for s in st2) / steps
-                pix = sum(s["rows"] for s in st2) / steps * d2.width
+                seg = sum(s["segments"] for s in st2) / steps / nshare
+                smp = sum(s["samples"] for s in st2) / steps / nshare
+                pix = sum(s["rows"] for s in st2) / steps * d2.width / nshare
                 ms = sum(s["ms_fused"] for s in st2) / steps
                 key = f"{sname}:{d2.width}x{d2.height}x{d2.spp_sqrt ** 2}"
-                roof = roofline(db, key, "k_fused", ms, seg, smp, pix)
+                roof = roofline(db, key, "k_fused", ms, seg, smp, pix,
+                                d2.width * d2.height * d2.spp_sqrt ** 2)
                 roof["avg_ms"] = round(ms, 4)
                 extra[name] = {
                     "workload": f"{sname} {d2.width}x{d2.height} {d2.spp_sqrt ** 2}spp maxdepth "
@@ -361,7 +393,7 @@ def main():
         if extra:
             line["extra_configs"] = extra
         cpu = None
-        if world_size == 1 and not args.no_cpu_baseline:
+        if world_size == 1 and not devices and not args.no_cpu_baseline:
             tree, cam, w, l = rt.demo_scene(args.scene)
             cam.Width, cam.SamplesPerPixel = args.width, args.spp
             if args.scene == "book1":

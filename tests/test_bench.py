@@ -1,0 +1,38 @@
+"""bench.py's contract line, in both multi-GPU drivers' shapes (small workloads).
+
+The single-process mode (--devices, rt_render_multi: the north_star's Go-host path) is
+rehearsed on one GPU with two shares on device 0; torchrun's one-process-per-GPU mode
+needs distinct GPUs (RCCL) and is covered by tests/test_distributed.py with gloo.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SMALL = ["--scene", "cornell", "--width", "160", "--spp", "64", "--steps", "2", "--warmup", "1",
+         "--no-cpu-baseline", "--no-extra-configs"]
+
+
+def _bench(*args):
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *SMALL, *args],
+                       capture_output=True, text=True, timeout=300, cwd=REPO)
+    return p
+
+
+def test_devices_mode_rejects_mismatched_count():
+    p = _bench("--gpus", "3", "--devices", "0,0")
+    assert p.returncode != 0 and "--devices must list --gpus devices" in p.stderr
+
+
+@pytest.mark.gpu
+def test_devices_mode_line(gpu):
+    p = _bench("--gpus", "2", "--devices", "0,0")
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 1  # distinct devices: both shares ran on device 0
+    assert "rt_render_multi" in line["config"]["parallelism"]
+    assert line["value"] > 0 and line["steps"] == 2
+    assert line["roofline"]["launches"] == 2
