@@ -4,8 +4,8 @@
 Headline workload (a "step"): one full render of the Cornell box (configs[1] = C2,
 main.go:278-320) at 800x800 with 1024 samples per pixel (32x32 strata,
 camera.go:211-213), MaxDepth 50 = 655.36 M camera samples, rows interleaved across
-ranks (row r -> rank r % N, camera.go:119-122) and gathered with one RCCL
-all_gather over xGMI.  The scene is uploaded to HBM during warmup; the timed region
+ranks (row r -> rank r % N, camera.go:119-122) and gathered to rank 0 with one
+RCCL gather over xGMI.  The scene is uploaded to HBM during warmup; the timed region
 holds only render + gather.
 
 After the headline, `extra_configs` times BASELINE configs C3 (book1), C4 (book2)
@@ -222,8 +222,8 @@ def main():
             st = scene.render_device(cam, buf.data_ptr(), seed=args.seed, device=local_rank,
                                      rank=rank, nranks=world_size, profile=prof,
                                      stream=stream.cuda_stream, mode=args.mode)
-            if world_size > 1:
-                dist.all_gather_into_tensor(gathered, buf)
+            if world_size > 1:  # one RCCL gather of the row tiles to rank 0
+                dist.gather(buf, list(gathered.split(buf.shape[0])) if rank == 0 else None, dst=0)
             return st
         t_first = None
         for i in range(warmup):
@@ -273,6 +273,10 @@ def main():
     if world_size > 1:
         dist.all_reduce(samples, op=dist.ReduceOp.SUM)
     total_samples = samples.item()
+    segments = torch.tensor([sum(s["segments"] for s in stats)], dtype=torch.float64, device=dev)
+    if world_size > 1:
+        dist.all_reduce(segments, op=dist.ReduceOp.SUM)
+    total_segments = segments.item()  # every rank's (rt_render_multi: every share's)
     line = None
     if rank == 0:
         seg = sum(s["segments"] for s in stats)
@@ -321,7 +325,7 @@ def main():
                        "mode": mode, "path_slots": stats[0]["path_slots"],
                        "chunk_samples": stats[0]["chunk_samples"],
                        "segments_per_sample": round(seg / max(smp, 1), 4),
-                       "Gsegments_per_s": round(seg / (elapsed * rank_share(world_size)) / 1e9, 3)},
+                       "Gsegments_per_s": round(total_segments / elapsed / 1e9, 3)},
             "roofline": roof,
             "wall_clock": {"scene_build_s": round(t_build, 3),
                            "first_step_s": None if t_first is None else round(t_first, 3),
@@ -407,11 +411,6 @@ def main():
         print(json.dumps(line), flush=True)
     if world_size > 1:
         dist.destroy_process_group()
-
-
-def rank_share(n):
-    """Segments are rank 0's; the rate per rank is seg / elapsed."""
-    return 1.0
 
 
 if __name__ == "__main__":

@@ -72,11 +72,14 @@ struct HostScene {
 struct DeviceScene;  // defined in the HIP translation unit
 struct RenderState;
 
-// Progress of the render in flight (rt_progress): written by the rendering
-// thread, read by any polling thread under `mu`.
+// Progress of the tracked render (rt_progress): written by the rendering thread,
+// read by any polling thread under `mu`.  One render is tracked at a time: the
+// rt_render / rt_render_multi call that finds `busy` clear claims it, and
+// only that render updates and clears it, so concurrent renders of one scene on
+// other devices neither reset nor finish another render's record.
 struct Progress {
   std::mutex mu;
-  int busy = 0;                 // 1 while a render is in flight
+  int busy = 0;                 // 1 while the tracked render is in flight
   int device = -1;
   uint64_t total = 0;           // samples of the current / last render
   uint64_t done = 0;            // samples of the last render once it returned
@@ -92,10 +95,18 @@ struct SlotState {
   RenderState* st = nullptr;
 };
 
+// A device's copy of the scene.  `mu` is held while it is uploaded, so uploads to
+// different devices run concurrently (rt_render_multi's share threads), and a
+// render on a device whose copy is being uploaded waits for that copy only.
+struct DeviceSlot {
+  std::mutex mu;
+  DeviceScene* ds = nullptr;  // null until the upload succeeded
+};
+
 struct Scene {
   HostScene h;
   std::mutex mu;                                    // guards the maps (not the renders)
-  std::map<int, DeviceScene*> devs;                 // per device ordinal, uploaded lazily
+  std::map<int, DeviceSlot*> devs;                  // per device ordinal, uploaded lazily
   std::map<std::pair<int, int>, SlotState*> slots;  // per (device, slot)
   std::mutex multi_mu;                              // one rt_render_multi at a time
   void* multi_buf = nullptr;                        // gather + image buffer on the first device

@@ -343,6 +343,81 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
   const f3 inv = tr.inv;
   int n = 0;
   for (; n < budget && cur != TRAV_DONE; ++n) {
+#ifndef RT_SPLIT_FETCH
+    if (W4 && !LDS) {
+      // One fetch per step for node and leaf lanes alike: 7 x 16 B from the node
+      // (nodes + 8 cur) or from the leaf's first record (leafprims + 4 first; the
+      // array is padded so the 3 F4 past the last record exist).  With the loads in
+      // each branch, a wave whose lanes are split between nodes and leaves waited
+      // for two dependent memory round trips per step; here it waits for one.
+      const bool leaf = (cur & LEAF_BIT) != 0u;
+      const uint32_t first = (cur >> 4) & 0x7FFFFFFu;
+      const F4* g = leaf ? sc.leafprims + 4 * (size_t)first : sc.nodes + 8 * (size_t)cur;
+      F4 v[7];
+#pragma unroll
+      for (int e = 0; e < 7; ++e) v[e] = ld_glb(g + e);
+      if (!leaf) {
+        const float tmax = tr.best.t;
+        float tn[4];
+        uint32_t ch[4];
+        const float Lx[4] = {v[0].x, v[0].y, v[0].z, v[0].w}, Hx[4] = {v[1].x, v[1].y, v[1].z, v[1].w};
+        const float Ly[4] = {v[2].x, v[2].y, v[2].z, v[2].w}, Hy[4] = {v[3].x, v[3].y, v[3].z, v[3].w};
+        const float Lz[4] = {v[4].x, v[4].y, v[4].z, v[4].w}, Hz[4] = {v[5].x, v[5].y, v[5].z, v[5].w};
+        const uint32_t C[4] = {fbits(v[6].x), fbits(v[6].y), fbits(v[6].z), fbits(v[6].w)};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float tx0 = (Lx[k] - o.x) * inv.x, tx1 = (Hx[k] - o.x) * inv.x;
+          const float ty0 = (Ly[k] - o.y) * inv.y, ty1 = (Hy[k] - o.y) * inv.y;
+          const float tz0 = (Lz[k] - o.z) * inv.z, tz1 = (Hz[k] - o.z) * inv.z;
+          const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
+          const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+          const bool h = t0 <= t1 * 1.00000024f && C[k] != CHILD_EMPTY;  // slab() semantics
+          tn[k] = h ? t0 : kInf;
+          ch[k] = C[k];
+        }
+        auto cx = [&](int a, int b) {
+          const bool sw = tn[b] < tn[a];
+          const float ta = tn[a], tb = tn[b];
+          const uint32_t ca = ch[a], cb = ch[b];
+          tn[a] = sw ? tb : ta;
+          tn[b] = sw ? ta : tb;
+          ch[a] = sw ? cb : ca;
+          ch[b] = sw ? ca : cb;
+        };
+        cx(0, 1);
+        cx(2, 3);
+        cx(0, 2);
+        cx(1, 3);
+        cx(1, 2);
+        if (tn[0] != kInf) {
+          if (tn[3] != kInf && sp < kStack) push(ch[3]);
+          if (tn[2] != kInf && sp < kStack) push(ch[2]);
+          if (tn[1] != kInf && sp < kStack) push(ch[1]);
+          cur = ch[0];
+          continue;
+        }
+      } else {
+        const uint32_t count = (cur & 15u) + 1u;
+        F4 rec[4] = {v[0], v[1], v[2], v[3]};
+        for (uint32_t k = 0;;) {
+          float t, u, vv;
+          uint32_t ref;
+          if (hit_record<FT>(rec, o, d, time, tmin, tr.best.t, t, u, vv, ref)) {
+            tr.best.t = t;
+            tr.best.u = u;
+            tr.best.v = vv;
+            tr.best.ref = ref;
+          }
+          if (++k >= count) break;
+          const F4* q = sc.leafprims + 4 * (size_t)(first + k);
+          for (int e = 0; e < 4; ++e) rec[e] = ld_glb(q + e);
+        }
+      }
+      if (sp == 0) cur = TRAV_DONE;
+      else cur = stack.pop(--sp);
+      continue;
+    }
+#endif
     if (!W4 && !(cur & LEAF_BIT)) {
       // BVH2 node (tiny scenes, see render_impl): both child boxes, nearer first
       const F4* g = LDS ? lnodes + 4 * cur : sc.nodes + 4 * (size_t)cur;
@@ -931,10 +1006,13 @@ RT_D uint32_t local_pixel(const Params& P, uint32_t chunk) {
   return chunk_pixel(P, chunk, sub);
 }
 // floor(v * 2^32) for |v| < 2^31: the integer part in the high word, the fraction
-// (exact: v - floor(v) loses no bits, and * 2^32 only moves the exponent) in the low
+// in the low.  v - floor(v) is exact except for v in (-2^-24, 0), where it rounds
+// to 1.0f; the fraction is capped at 1 - 2^-24 so its conversion stays in range
+// (those samples count as -2^-24: error below 2^-24, still a fixed function of v,
+// so the sums stay order-independent); * 2^32 only moves the exponent.
 RT_D unsigned long long to_fixed(float v) {
   const float hi = floorf(v);
-  const uint32_t lo = (uint32_t)((v - hi) * 4294967296.0f);
+  const uint32_t lo = (uint32_t)(fminf(v - hi, 0x1.fffffep-1f) * 4294967296.0f);
   return ((unsigned long long)(uint32_t)(int32_t)hi << 32) | lo;
 }
 // a sample with a channel outside the fixed-point range or non-finite (rare): every

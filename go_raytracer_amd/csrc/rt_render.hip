@@ -437,7 +437,20 @@ struct RenderState {
   }
 };
 
+// Restores the calling thread's current device on scope exit: every ABI entry that
+// switches devices leaves the caller's (e.g. torch's) current device as it found it.
+struct DeviceGuard {
+  int prev = -1;
+  DeviceGuard() {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
 void release_device(Scene* s) {
+  DeviceGuard dg;
   std::lock_guard<std::mutex> lk(s->mu);
   for (auto& kv : s->slots) {
     if (kv.second->st) {
@@ -448,7 +461,10 @@ void release_device(Scene* s) {
   }
   s->slots.clear();
   for (auto& kv : s->devs) {
-    (void)hipSetDevice(kv.first);
+    if (kv.second->ds) {
+      (void)hipSetDevice(kv.first);
+      delete kv.second->ds;
+    }
     delete kv.second;
   }
   s->devs.clear();
@@ -538,13 +554,21 @@ static void make_record(const HostScene& h, uint32_t ref, F4* r) {
 }
 
 // the scene's device copy on `device` (uploaded on first use, then shared by every
-// slot on that device; read-only while rendering)
+// slot on that device; read-only while rendering).  The scene-wide lock covers the
+// map lookup only; the upload holds its device's own lock, so first renders on
+// different devices upload concurrently.  Called with `device` current.
 static int upload_scene(const Scene* s, DeviceScene* ds);
 static int ensure_scene(Scene* s, int device, DeviceScene** out) {
-  std::lock_guard<std::mutex> lk(s->mu);
-  auto it = s->devs.find(device);
-  if (it != s->devs.end()) {
-    *out = it->second;
+  DeviceSlot* slot;
+  {
+    std::lock_guard<std::mutex> lk(s->mu);
+    DeviceSlot*& sl = s->devs[device];
+    if (!sl) sl = new DeviceSlot();
+    slot = sl;
+  }
+  std::lock_guard<std::mutex> up(slot->mu);
+  if (slot->ds) {
+    *out = slot->ds;
     return RT_OK;
   }
   DeviceScene* ds = new DeviceScene();
@@ -558,7 +582,7 @@ static int ensure_scene(Scene* s, int device, DeviceScene** out) {
     delete ds;
     return rc;
   }
-  s->devs[device] = ds;
+  slot->ds = ds;
   *out = ds;
   return RT_OK;
 }
@@ -605,6 +629,7 @@ static int upload_scene(const Scene* s, DeviceScene* ds) {
   {
     std::vector<F4> recs, lrecs;
     build_leaf_records(h, recs);
+    recs.resize(recs.size() + 4, F4{0, 0, 0, 0});  // trav_steps' 7-F4 fetch past the last record
     UP(recs, leafprims);
     build_light_records(h, lrecs);
     UP(lrecs, light_recs);
@@ -837,6 +862,7 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     return set_error(RT_ERR_DEVICE, "rt_render: no HIP device available");
   if (o.device < 0 || o.device >= ndev)
     return set_error(RT_ERR_INVALID, "rt_render: device %d of %d", o.device, ndev);
+  DeviceGuard dg;  // the caller's current device is restored on every return
   HIP_OK(hipSetDevice(o.device));
   Scene* s = &scene->s;
   DeviceScene* ds = nullptr;
@@ -849,7 +875,6 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     slot = sl;
   }
   std::lock_guard<std::mutex> inflight(slot->mu);  // one render per (scene, device, slot)
-  const bool track = slot_id == 0;  // rt_progress follows rt_render; rt_render_multi sets its own
 
   const uint32_t W = (uint32_t)cd.width, H = (uint32_t)cd.height;
   const uint32_t rows = H > (uint32_t)o.rank ? (H - (uint32_t)o.rank + o.nranks - 1) / o.nranks : 0;
@@ -1101,6 +1126,16 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     st->prog_events.push_back(e);
   }
+  // rt_progress follows one render per scene: an rt_render call (slot 0) claims the
+  // record when no other render holds it (rt_render_multi claims it for its shares)
+  bool track = false;
+  if (slot_id == 0) {
+    std::lock_guard<std::mutex> lk(s->prog.mu);
+    if (!s->prog.busy) {  // claimed: no return before prog_done below releases it
+      s->prog.busy = 1;
+      track = true;
+    }
+  }
   if (track) {
     std::lock_guard<std::mutex> lk(s->prog.mu);
     s->prog.total = (uint64_t)npix * ss;
@@ -1311,6 +1346,7 @@ static int render_multi(rt_scene* scene, const rt_camera* cam, const rt_render_o
   const uint32_t rows_per = (H + N - 1) / N;
   const size_t gather_floats = (size_t)N * rows_per * W * 3, img_floats = (size_t)H * W * 3;
   const int d0 = devices[0];
+  DeviceGuard dg;  // the caller's current device is restored on every return
   HIP_OK(hipSetDevice(d0));
   const size_t need = (gather_floats + img_floats) * sizeof(float);
   if (!s->multi_buf || s->multi_dev != d0 || s->multi_bytes < need) {
@@ -1326,24 +1362,42 @@ static int render_multi(rt_scene* scene, const rt_camera* cam, const rt_render_o
   }
   float* gbuf = (float*)s->multi_buf;
   float* img = out_dev ? out_dev : gbuf + gather_floats;
-  for (int i = 1; i < n; ++i)  // xGMI peer access both ways (already enabled is fine)
-    if (devices[i] != d0) {
-      int can = 0;
-      if (hipDeviceCanAccessPeer(&can, devices[i], d0) == hipSuccess && can) {
-        HIP_OK(hipSetDevice(devices[i]));
-        (void)hipDeviceEnablePeerAccess(d0, 0);
-        HIP_OK(hipSetDevice(d0));
-        (void)hipDeviceEnablePeerAccess(devices[i], 0);
-      }
-      (void)hipGetLastError();
+  // xGMI peer access both ways.  "Already enabled" is success; any other failure is
+  // an error (the copies would silently fall back to staging through host memory).
+  // Devices that report no peer path copy through the runtime's staged path.
+  auto enable_peer = [](int from, int to) -> int {
+    HIP_OK(hipSetDevice(from));
+    const hipError_t e = hipDeviceEnablePeerAccess(to, 0);
+    if (e == hipErrorPeerAccessAlreadyEnabled) {
+      (void)hipGetLastError();  // clear the sticky "already enabled" status
+      return RT_OK;
     }
+    if (e != hipSuccess)
+      return set_error(RT_ERR_DEVICE, "rt_render_multi: peer access %d -> %d: %s", from, to,
+                       hipGetErrorString(e));
+    return RT_OK;
+  };
+  for (int i = 1; i < n; ++i)
+    if (devices[i] != d0) {
+      int can_a = 0, can_b = 0;
+      HIP_OK(hipDeviceCanAccessPeer(&can_a, devices[i], d0));
+      HIP_OK(hipDeviceCanAccessPeer(&can_b, d0, devices[i]));
+      if (can_a && (rc = enable_peer(devices[i], d0))) return rc;
+      if (can_b && (rc = enable_peer(d0, devices[i]))) return rc;
+    }
+  HIP_OK(hipSetDevice(d0));
+  // rt_progress: this call's shares are the tracked render unless another holds it
+  bool track = false;
   {
     std::lock_guard<std::mutex> lk(s->prog.mu);
-    s->prog.total = (uint64_t)H * W * cd.spp_sqrt * cd.spp_sqrt;
-    s->prog.done = 0;
-    s->prog.events.clear();
-    s->prog.cum.clear();
-    s->prog.busy = 1;
+    if (!s->prog.busy) {
+      track = true;
+      s->prog.total = (uint64_t)H * W * cd.spp_sqrt * cd.spp_sqrt;
+      s->prog.done = 0;
+      s->prog.events.clear();
+      s->prog.cum.clear();
+      s->prog.busy = 1;
+    }
   }
   std::vector<rt_stats> st(n);
   std::vector<int> rcs(n, RT_OK);
@@ -1361,10 +1415,17 @@ static int render_multi(rt_scene* scene, const rt_camera* cam, const rt_render_o
       if (rcs[i] != RT_OK) errs[i] = rt_last_error();
     });
   for (auto& t : th) t.join();
-  {
-    std::lock_guard<std::mutex> lk(s->prog.mu);
-    s->prog.busy = 0;
-  }
+  struct ProgressDone {  // every return path below ends the tracked state
+    Progress& p;
+    bool track;
+    bool ok = false;
+    ~ProgressDone() {
+      if (!track) return;
+      std::lock_guard<std::mutex> lk(p.mu);
+      if (ok) p.done = p.total;
+      p.busy = 0;
+    }
+  } prog_done{s->prog, track};
   for (int i = 0; i < n; ++i)
     if (rcs[i] != RT_OK) return set_error(rcs[i], "rt_render_multi share %d: %s", i, errs[i].c_str());
   HIP_OK(hipSetDevice(d0));
@@ -1375,11 +1436,8 @@ static int render_multi(rt_scene* scene, const rt_camera* cam, const rt_render_o
     if (out_host)
       HIP_OK(hipMemcpy(out_host, img, img_floats * sizeof(float), hipMemcpyDeviceToHost));
   }
-  HIP_OK(hipDeviceSynchronize());
-  {
-    std::lock_guard<std::mutex> lk(s->prog.mu);
-    s->prog.done = s->prog.total;
-  }
+  HIP_OK(hipStreamSynchronize((hipStream_t)0));
+  prog_done.ok = true;
   if (stats) {
     memset(stats, 0, sizeof *stats);
     *stats = st[0];

@@ -70,6 +70,26 @@ def test_empty_world_is_background(rt, oracle, gpu):
     assert np.allclose(img, ref, rtol=0, atol=1e-6)
 
 
+def test_small_negative_samples_in_fixed_point(rt, gpu):
+    """Pixel sums take each sample as floor(v * 2^32) in int64 (rt_path.h to_fixed).
+    Negative samples work like positive ones; the one corner is (-2^-24, 0), where
+    v - floor(v) rounds to 1.0f in fp32: those samples are taken as -2^-24 (a defined
+    conversion, error below 2^-24), never as an out-of-range float-to-int cast."""
+    t = rt.Tree(1)
+    world = t.list()
+    bg = (-1e-30, -3e-9, -0.25)
+    cam = rt.Camera(Width=8, SamplesPerPixel=9, Background=bg)
+    with rt.Scene(t, world, -1) as sc:
+        img, st = sc.render(cam, seed=1)
+    assert st["overflow_samples"] == 0
+    assert np.isfinite(img).all()
+    ulp24 = 2.0 ** -24
+    assert np.all(np.abs(img[..., 0].astype(np.float64) - bg[0]) <= ulp24)
+    assert np.all(np.abs(img[..., 1].astype(np.float64) - bg[1]) <= ulp24)
+    assert np.all(img[..., 0] <= 0) and np.all(img[..., 1] <= 0)
+    assert np.all(img[..., 2] == np.float32(-0.25))  # exact in fixed point
+
+
 def test_world_without_lights_list(rt, oracle, gpu):
     """lights = nil-equivalent (-1): the mixture pdf's light half follows the
     reference's empty-list rules (hittable.go:89-103)."""

@@ -185,6 +185,62 @@ def test_render_multi_device_output(rt, gpu):
     assert np.array_equal(buf.cpu().numpy(), ref, equal_nan=True)
 
 
+def test_concurrent_scenes_on_one_device(rt, gpu):
+    """rt_render is re-entrant across scene handles (rt_abi.h threading rules): two
+    host threads rendering two different scenes on device 0 at once (ctypes drops the
+    GIL for the call) get the same bits as serial renders; meanwhile a third thread
+    renders one of the scenes through rt_render_multi's shares, and each scene's
+    device copy is uploaded once, under its own device lock (rt_render.hip
+    ensure_scene), while the other scene's upload and render run."""
+    import threading
+    jobs = [_scene(rt, "cornell", 64, 64), _scene(rt, "book2", 48, 64)]
+    serial = []
+    for t, cam, w, l in jobs:
+        with rt.Scene(t, w, l) as sc:
+            serial.append(sc.render(cam, seed=11)[0])
+    scenes = [rt.Scene(t, w, l) for t, _, w, l in jobs]
+    out = {}
+    def run(i, multi=False):
+        cam = jobs[i][1]
+        for rep in range(3):
+            img = (scenes[i].render_multi(cam, [0, 0], seed=11)[0] if multi
+                   else scenes[i].render(cam, seed=11)[0])
+            out[(i, multi, rep)] = img
+    th = [threading.Thread(target=run, args=(0,)), threading.Thread(target=run, args=(1,)),
+          threading.Thread(target=run, args=(1, True))]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(120)
+    for sc in scenes:
+        sc.close()
+    assert len(out) == 9
+    for (i, multi, rep), img in out.items():
+        assert np.array_equal(img, serial[i], equal_nan=True), (i, multi, rep)
+
+
+@pytest.mark.skipif("__import__('go_raytracer_amd').device_count() < 2")
+def test_render_multi_distinct_devices(rt, gpu):
+    """rt_render_multi over two distinct GPUs (peer access, peer copies into the
+    gather buffer on devices[0], per-device scene uploads, remote de-interleave):
+    [0, 1] and [1, 0] equal a one-device render bit for bit, also into a device
+    buffer on devices[0].  Runs on boxes with two or more GPUs."""
+    import torch
+    t, cam, w, l = _scene(rt, "book2", 97, 16)
+    d = cam.derived()
+    with rt.Scene(t, w, l) as sc:
+        one, _ = sc.render(cam, seed=6)
+        a, _ = sc.render_multi(cam, [0, 1], seed=6)
+        b, _ = sc.render_multi(cam, [1, 0], seed=6)
+        buf = torch.zeros((d.height, d.width, 3), dtype=torch.float32, device="cuda:1")
+        sc.render_multi_device(cam, [1, 0, 1], buf.data_ptr(), seed=6)
+        torch.cuda.synchronize(1)
+        c = buf.cpu().numpy()
+    assert np.array_equal(one, a, equal_nan=True)
+    assert np.array_equal(one, b, equal_nan=True)
+    assert np.array_equal(one, c, equal_nan=True)
+
+
 def test_c1_full_size_parity(rt, oracle, gpu):
     """BASELINE configs[0] (C1: quads, 400x400, 64 spp, main.go:220-247) at full size:
     10.24 M samples on the GPU against the fp64 oracle (the reference runs it on the
