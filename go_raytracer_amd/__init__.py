@@ -415,6 +415,16 @@ class Scene:
         check(lib().rt_scene_export_prim_bounds(self._p, bounds.ctypes.data or None, C.byref(n)))
         return nodes, refs, int(root.value), bounds
 
+    def export_bvh8(self):
+        """(nodes uint32 [N, 32] in the rt_device.h BVH8 layout, refs8 uint32 [R])."""
+        nn, nr = C.c_int32(), C.c_int32()
+        check(lib().rt_scene_export_bvh8(self._p, None, C.byref(nn), None, C.byref(nr)))
+        nodes = np.zeros((max(nn.value, 0), 32), np.uint32)
+        refs = np.zeros(max(nr.value, 0), np.uint32)
+        check(lib().rt_scene_export_bvh8(self._p, nodes.ctypes.data or None, C.byref(nn),
+                                         refs.ctypes.data or None, C.byref(nr)))
+        return nodes, refs
+
     MODES = {"auto": 0, "wavefront": 1, "fused": 2}
 
     @staticmethod
@@ -461,20 +471,21 @@ class Scene:
         return out, res
 
     def render_multi(self, camera, devices, seed=1, path_slots=0, chunk=0, profile=False,
-                     mode="auto"):
+                     mode="auto", rccl=False):
         """The whole image over several devices (rt_render_multi: row r on
-        devices[r % n], peer-copied to devices[0]) -> (float32 [H, W, 3], stats)."""
+        devices[r % n], gathered to devices[0] by peer copies, or by one RCCL
+        ncclGather with rccl=True) -> (float32 [H, W, 3], stats)."""
         d = camera.derived()
         out = np.zeros((d.height, d.width, 3), np.float32)
         st = _multi(self, camera, devices, (out.ctypes.data, False), seed, path_slots, chunk,
-                    profile, mode)
+                    profile, mode, rccl)
         return out, st
 
     def render_multi_device(self, camera, devices, out_ptr, seed=1, path_slots=0, chunk=0,
-                            profile=False, mode="auto"):
+                            profile=False, mode="auto", rccl=False):
         """rt_render_multi_device: the whole image into a device buffer on devices[0]."""
         return _multi(self, camera, devices, (out_ptr, True), seed, path_slots, chunk, profile,
-                      mode)
+                      mode, rccl)
 
     def render_device(self, camera, out_ptr, seed=1, device=0, rank=0, nranks=1, path_slots=0,
                       chunk=0, profile=False, stream=None, mode="auto"):
@@ -487,12 +498,14 @@ class Scene:
         return {f: getattr(st, f) for f, _ in RtStats._fields_}
 
 
-def _multi(scene, camera, devices, out_ptr, seed, path_slots, chunk, profile, mode):
+def _multi(scene, camera, devices, out_ptr, seed, path_slots, chunk, profile, mode, rccl=False):
     devs = (C.c_int32 * len(devices))(*[int(d) for d in devices])
     st = RtStats()
     c = camera.to_c()
     o = scene._opts(seed, int(devices[0]) if len(devices) else 0, 0, 1, path_slots, chunk,
                     profile, None, mode)
+    if rccl:
+        o.flags |= _lib.RT_FLAG_GATHER_RCCL
     fn = lib().rt_render_multi_device if out_ptr[1] else lib().rt_render_multi
     check(fn(scene._p, C.byref(c), C.byref(o), devs, len(devices), C.c_void_p(out_ptr[0]),
              C.byref(st)))

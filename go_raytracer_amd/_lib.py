@@ -24,6 +24,7 @@ RT_NOISE_PERLIN, RT_NOISE_MARBLE, RT_NOISE_TURBULENT = 1, 2, 3
 (RT_NODE_LIST, RT_NODE_BVH, RT_NODE_SPHERE, RT_NODE_QUAD, RT_NODE_TRIANGLE,
  RT_NODE_TRANSLATE, RT_NODE_ROTATE_Y, RT_NODE_MEDIUM) = range(8)
 RT_FLAG_PROFILE = 1
+RT_FLAG_GATHER_RCCL = 2  # rt_render_multi: one RCCL ncclGather instead of peer copies
 RT_FT_SPHERE, RT_FT_TRI, RT_FT_METAL, RT_FT_DIEL = 1, 2, 4, 8
 RT_FT_MEDIA, RT_FT_CHECKER, RT_FT_IMAGE, RT_FT_NOISE = 16, 32, 64, 128
 RT_MODE_AUTO, RT_MODE_WAVEFRONT, RT_MODE_FUSED = 0, 1, 2
@@ -172,6 +173,8 @@ SIGNATURES = {
     "rt_scene_info_get": (_I, [_P, C.POINTER(RtSceneInfo)]),
     "rt_scene_export_bvh": (_I, [_P, C.c_void_p, C.POINTER(C.c_int32), C.c_void_p,
                                  C.POINTER(C.c_int32), C.POINTER(C.c_uint32)]),
+    "rt_scene_export_bvh8": (_I, [_P, C.c_void_p, C.POINTER(C.c_int32), C.c_void_p,
+                                  C.POINTER(C.c_int32)]),
     "rt_scene_export_prim_bounds": (_I, [_P, C.c_void_p, C.POINTER(C.c_int32)]),
     "rt_render": (_I, [_P, C.POINTER(RtCamera), C.POINTER(RtRenderOpts), C.c_void_p,
                        C.POINTER(RtStats)]),

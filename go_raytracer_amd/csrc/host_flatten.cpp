@@ -524,6 +524,18 @@ int flatten_scene(const Tree& t, int world, int lights, HostScene& out) {
   if (timing)
     fprintf(stderr, "[rt] build_bvh (%s) %.3f s\n", on_device ? "device" : "host",
             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+  if (rc != RT_OK) return rc;
+  // the wide tree (host_bvh8.cpp), opt-in: RT_BVH8=1 at scene creation.  Measured
+  // slower than the BVH4 on C4/C5, kept for A/B and further work
+  const char* b8 = getenv("RT_BVH8");
+  if (b8 && atoi(b8) != 0 && out.refs.size() >= kBvh8MinRefs) {
+    t0 = std::chrono::steady_clock::now();
+    rc = build_bvh8(out);
+    if (timing)
+      fprintf(stderr, "[rt] build_bvh8 %.3f s (%zu nodes)\n",
+              std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(),
+              out.nodes8.size() / 8);
+  }
   return rc;
 }
 

@@ -151,6 +151,17 @@ int rt_scene_export_bvh(const rt_scene* sc, float* nodes, int32_t* n_nodes, uint
   return RT_OK;
 }
 
+int rt_scene_export_bvh8(const rt_scene* sc, float* nodes, int32_t* n_nodes, uint32_t* refs8,
+                         int32_t* n_refs8) {
+  if (!sc) return set_error(RT_ERR_INVALID, "rt_scene_export_bvh8: null");
+  const rt::HostScene& h = sc->s.h;
+  if (n_nodes) *n_nodes = (int32_t)(h.nodes8.size() / 8);
+  if (n_refs8) *n_refs8 = (int32_t)h.refs8.size();
+  if (nodes && !h.nodes8.empty()) memcpy(nodes, h.nodes8.data(), h.nodes8.size() * 16);
+  if (refs8 && !h.refs8.empty()) memcpy(refs8, h.refs8.data(), h.refs8.size() * 4);
+  return RT_OK;
+}
+
 int rt_scene_export_prim_bounds(const rt_scene* sc, float* bounds, int32_t* n) {
   if (!sc) return set_error(RT_ERR_INVALID, "rt_scene_export_prim_bounds: null");
   const rt::HostScene& h = sc->s.h;

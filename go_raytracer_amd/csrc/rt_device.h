@@ -40,6 +40,14 @@ inline constexpr uint32_t leaf_code(uint32_t first, uint32_t count) {
 // child code: inner BVH4 node index, leaf code (LEAF_BIT, as BVH2), or CHILD_EMPTY
 constexpr uint32_t CHILD_EMPTY = 0xFFFFFFFEu;
 
+// ---- BVH8 node: eight children, 16-bit planes relative to the node's box (128 B)
+//  f4[0] = origin.xyz | biased exponents (bytes 0-2: plane = origin + q * 2^(E-127))
+//  f4[1] = child_base, leaf_base, meta of slots 0-3, meta of slots 4-7
+//          meta byte: 0xFF empty; 0x80 | r inner child = node child_base + r;
+//          else leaf: records leaf_base + (m & 31), count ((m >> 5) & 3) + 1
+//  f4[2..7] = qlo.x, qhi.x, qlo.y, qhi.y, qlo.z, qhi.z (uint16, slot k in halfword k)
+// Built by host_bvh8.cpp for scenes of >= kBvh8MinRefs leaf entries.
+
 // ---- per-type primitive records ------------------------------------------
 // sphere (objects.go:14-37): sph_cr = center@t0 | radius ; sph_mv = motion | mat bits
 //   sph_uv = cos,sin of the baked Y rotation (UV is computed in object space, objects.go:113)
@@ -120,6 +128,8 @@ struct DevScene {
   const F4* nodes;      // the tree this launch traverses (BVH4, or BVH2 for tiny scenes)
   const uint32_t* refs;
   const F4* leafprims;  // 4 x F4 per leaf entry, parallel to refs (see "leaf records")
+  const F4* nodes8;     // BVH8 (host_bvh8.cpp layout), root = node 0; null when not built
+  const F4* recs8;      // the BVH8's leaf records (leaf record format), in node order
   uint32_t root;
   int32_t n_nodes;
   const DevMedium* media;

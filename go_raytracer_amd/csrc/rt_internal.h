@@ -49,6 +49,8 @@ struct HostScene {
   std::vector<F4> nodes;     // BVH2, 4 per node (export / structural tests)
   std::vector<F4> nodes4;    // BVH4 the kernels traverse, 8 per node (rt_device.h)
   uint32_t root4 = PRIM_NONE;
+  std::vector<F4> nodes8;    // BVH8, 8 F4 per node, root = node 0 (large scenes, host_bvh8.cpp)
+  std::vector<uint32_t> refs8;  // the BVH8's leaf records in node order (prim refs)
   std::vector<uint32_t> refs;
   uint32_t root = PRIM_NONE;
   std::vector<float> prim_bounds;  // 6 per world ref (export/tests)
@@ -112,6 +114,7 @@ struct Scene {
   void* multi_buf = nullptr;                        // gather + image buffer on the first device
   size_t multi_bytes = 0;
   int multi_dev = -1;
+  void* rccl = nullptr;                             // RCCL gather state (rt_render.hip RcclGather)
   Progress prog;
 };
 
@@ -120,6 +123,9 @@ int flatten_scene(const Tree& t, int world, int lights, HostScene& out);
 // host_bvh.cpp
 int build_bvh(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi,
               const std::vector<uint32_t>& prims);
+// host_bvh8.cpp: the BVH8 of s.nodes (the binary tree) -> s.nodes8 / s.refs8
+constexpr size_t kBvh8MinRefs = 1024;
+int build_bvh8(HostScene& s);
 // rt_build.hip: the same outputs as build_bvh, built by PLOC on `device` (-1: the calling
 // thread's current device; the current device is restored on return)
 int build_bvh_device(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi,

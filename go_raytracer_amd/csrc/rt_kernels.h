@@ -204,6 +204,31 @@ RT_D bool hit_tri(const DevScene& sc, uint32_t i, f3 o, f3 d, float tmin, float 
   return true;
 }
 
+// The closest triangle hit's t, u, v re-evaluated in fp64 (Triangle.Hit objects.go:408-461
+// on the same fp32 ray and vertex data).  The traversal decides WHICH triangle and
+// whether it is hit in fp32; this only refines the values the shading reads.  In
+// fp32, u and v carry an absolute error of ~eps * |o - v0| / |edge| (the triple
+// products cancel), i.e. ~1e-5 for rays crossing a 1M-triangle mesh: the smooth
+// normal interpolated from them is off by that much, and on chains of metal bounces
+// the fp32 path drifted away from the fp64 reference's (tools/fork_probe.py: every
+// forked sample of C5 forked after 2-14 bounces of accumulated drift).
+RT_D void refine_tri_hit(const DevScene& sc, uint32_t idx, f3 o, f3 d, float& t_io, float& u_io,
+                         float& v_io) {
+  const F4* tr = sc.tri + 3 * (size_t)idx;
+  const F4 V0 = tr[0], E0 = tr[1], E1 = tr[2];
+  const double dx = d.x, dy = d.y, dz = d.z;
+  const double ax = E0.x, ay = E0.y, az = E0.z, bx = E1.x, by = E1.y, bz = E1.z;
+  const double px = dy * bz - dz * by, py = dz * bx - dx * bz, pz = dx * by - dy * bx;  // d x e1
+  const double det = ax * px + ay * py + az * pz;
+  double inv = __builtin_amdgcn_rcp(det);
+  inv = fma(inv, fma(-det, inv, 1.0), inv);
+  const double tx = (double)o.x - V0.x, ty = (double)o.y - V0.y, tz = (double)o.z - V0.z;
+  const double qx = ty * az - tz * ay, qy = tz * ax - tx * az, qz = tx * ay - ty * ax;  // tvec x e0
+  u_io = (float)((tx * px + ty * py + tz * pz) * inv);
+  v_io = (float)((dx * qx + dy * qy + dz * qz) * inv);
+  t_io = (float)((bx * qx + by * qy + bz * qz) * inv);
+}
+
 RT_D bool hit_prim(const DevScene& sc, uint32_t ref, f3 o, f3 d, float time, float tmin,
                    float tmax, float& t, float& u, float& v) {
   uint32_t type = ref >> 30, idx = ref & 0x3FFFFFFFu;

@@ -345,18 +345,21 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
   for (; n < budget && cur != TRAV_DONE; ++n) {
 #ifndef RT_SPLIT_FETCH
     if (W4 && !LDS) {
-      // One fetch per step for node and leaf lanes alike: 7 x 16 B from the node
-      // (nodes + 8 cur) or from the leaf's first record (leafprims + 4 first; the
-      // array is padded so the 3 F4 past the last record exist).  With the loads in
-      // each branch, a wave whose lanes are split between nodes and leaves waited
-      // for two dependent memory round trips per step; here it waits for one.
+      // One fetch per step for node and leaf lanes alike: the node (nodes + 8 cur,
+      // 7 x 16 B) or the leaf's first record (leafprims + 4 first, 4 x 16 B), issued
+      // together before either is used.  With the loads inside each branch, a wave
+      // whose lanes are split between nodes and leaves waited for two dependent
+      // memory round trips per step; here it waits for one (C3 -1.7 %, C4 -4.9 %,
+      // C5 -2.8 %, profiles/r3_unified_fetch_ab.jsonl).
       const bool leaf = (cur & LEAF_BIT) != 0u;
       const uint32_t first = (cur >> 4) & 0x7FFFFFFu;
       const F4* g = leaf ? sc.leafprims + 4 * (size_t)first : sc.nodes + 8 * (size_t)cur;
       F4 v[7];
 #pragma unroll
-      for (int e = 0; e < 7; ++e) v[e] = ld_glb(g + e);
+      for (int e = 0; e < 4; ++e) v[e] = ld_glb(g + e);
       if (!leaf) {
+#pragma unroll
+        for (int e = 4; e < 7; ++e) v[e] = ld_glb(g + e);
         const float tmax = tr.best.t;
         float tn[4];
         uint32_t ch[4];
@@ -518,6 +521,126 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
   tr.cur = cur;
   tr.sp = sp;
   tr.top = top;
+  return n;
+}
+
+// ---- BVH8 (large scenes, host_bvh8.cpp layout, rt_device.h "BVH8 node") ----
+// A child slot's traversal code from its meta byte: inner node child_base + rank, or
+// a leaf code over recs8 (the same LEAF_BIT format as the BVH4's leaves).
+RT_D uint32_t bvh8_code(uint32_t m, uint32_t child_base, uint32_t leaf_base) {
+  return (m & 0x80u) ? child_base + (m & 7u)
+                     : LEAF_BIT | ((leaf_base + (m & 31u)) << 4) | ((m >> 5) & 3u);
+}
+RT_D uint32_t bvh8_meta(uint32_t m0, uint32_t m1, uint32_t k) {
+  return (uint32_t)((((unsigned long long)m1 << 32) | m0) >> (8u * k)) & 0xFFu;
+}
+// Resumable closest-hit traversal of the BVH8 (same contract as trav_steps).  A
+// node step fetches one 128-B line per lane and tests eight children: each plane
+// is t = (origin + q * 2^e - o) * inv, evaluated as fma(q, 2^e * inv, (origin - o)
+// * inv) (2^e * inv is exact); the boxes carry one quantum of padding and the hit
+// test 4 ulp of slack on the exit distance, which cover this form's rounding.
+// The hit children's entry distances are sorted as keys (t0 bits with the slot in
+// the low 3 bits: t0 >= tmin > 0, so the bits order like the floats) by a
+// 19-comparator network of integer min/max; the nearest is visited next, the rest
+// pushed farthest first.  Leaf steps fetch the record (64 B) only.
+template <uint32_t FT>
+RT_D int trav_steps8(const DevScene& sc, const TravStack& stack, f3 o, f3 d, float time,
+                     float tmin, Trav& tr, int budget) {
+  uint32_t cur = tr.cur;
+  int sp = tr.sp;
+  const f3 inv = tr.inv;
+  const bool negx = inv.x < 0.0f, negy = inv.y < 0.0f, negz = inv.z < 0.0f;
+  int n = 0;
+  for (; n < budget && cur != TRAV_DONE; ++n) {
+    const bool leaf = (cur & LEAF_BIT) != 0u;
+    const uint32_t first = (cur >> 4) & 0x7FFFFFFu;
+    const F4* g = leaf ? sc.recs8 + 4 * (size_t)first : sc.nodes8 + 8 * (size_t)cur;
+    F4 v[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = ld_glb(g + e);
+    if (!leaf) {
+#pragma unroll
+      for (int e = 4; e < 8; ++e) v[e] = ld_glb(g + e);
+      const uint32_t ex = fbits(v[0].w);
+      const float scx = bitsf((ex & 0xFFu) << 23) * inv.x;
+      const float scy = bitsf(((ex >> 8) & 0xFFu) << 23) * inv.y;
+      const float scz = bitsf(((ex >> 16) & 0xFFu) << 23) * inv.z;
+      const float bx = (v[0].x - o.x) * inv.x, by = (v[0].y - o.y) * inv.y,
+                  bz = (v[0].z - o.z) * inv.z;
+      const uint32_t child_base = fbits(v[1].x), leaf_base = fbits(v[1].y);
+      const uint32_t m0 = fbits(v[1].z), m1 = fbits(v[1].w);
+      const uint32_t LX[4] = {fbits(v[2].x), fbits(v[2].y), fbits(v[2].z), fbits(v[2].w)};
+      const uint32_t HX[4] = {fbits(v[3].x), fbits(v[3].y), fbits(v[3].z), fbits(v[3].w)};
+      const uint32_t LY[4] = {fbits(v[4].x), fbits(v[4].y), fbits(v[4].z), fbits(v[4].w)};
+      const uint32_t HY[4] = {fbits(v[5].x), fbits(v[5].y), fbits(v[5].z), fbits(v[5].w)};
+      const uint32_t LZ[4] = {fbits(v[6].x), fbits(v[6].y), fbits(v[6].z), fbits(v[6].w)};
+      const uint32_t HZ[4] = {fbits(v[7].x), fbits(v[7].y), fbits(v[7].z), fbits(v[7].w)};
+      // entry / exit planes by the ray's direction signs, selected as whole words
+      uint32_t NX[4], FX[4], NY[4], FY[4], NZ[4], FZ[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        NX[j] = negx ? HX[j] : LX[j];
+        FX[j] = negx ? LX[j] : HX[j];
+        NY[j] = negy ? HY[j] : LY[j];
+        FY[j] = negy ? LY[j] : HY[j];
+        NZ[j] = negz ? HZ[j] : LZ[j];
+        FZ[j] = negz ? LZ[j] : HZ[j];
+      }
+      const float tmax = tr.best.t;
+      uint32_t key[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int j = k >> 1, sh = (k & 1) * 16;
+        auto q = [&](uint32_t w) { return (float)((w >> sh) & 0xFFFFu); };
+        const float t0 = fmaxf(fmaxf(fmaf(q(NX[j]), scx, bx), fmaf(q(NY[j]), scy, by)),
+                               fmaxf(fmaf(q(NZ[j]), scz, bz), tmin));
+        const float t1 = fminf(fminf(fmaf(q(FX[j]), scx, bx), fmaf(q(FY[j]), scy, by)),
+                               fminf(fmaf(q(FZ[j]), scz, bz), tmax));
+        const uint32_t m = ((k < 4 ? m0 : m1) >> (8 * (k & 3))) & 0xFFu;
+        const bool h = t0 <= t1 * 1.0000005f && m != 0xFFu;
+        key[k] = h ? (fbits(t0) & ~7u) | (uint32_t)k : 0xFFFFFFFFu;
+      }
+      auto cx = [&](int a, int b) {
+        const uint32_t lo = min(key[a], key[b]), hi = max(key[a], key[b]);
+        key[a] = lo;
+        key[b] = hi;
+      };
+      cx(0, 1), cx(2, 3), cx(4, 5), cx(6, 7);
+      cx(0, 2), cx(1, 3), cx(4, 6), cx(5, 7);
+      cx(1, 2), cx(5, 6);
+      cx(0, 4), cx(1, 5), cx(2, 6), cx(3, 7);
+      cx(2, 4), cx(3, 5);
+      cx(1, 2), cx(3, 4), cx(5, 6);
+      if (key[0] != 0xFFFFFFFFu) {
+#pragma unroll
+        for (int i = 7; i >= 1; --i)
+          if (key[i] != 0xFFFFFFFFu && sp < kStack)
+            stack.push(sp++, bvh8_code(bvh8_meta(m0, m1, key[i] & 7u), child_base, leaf_base));
+        cur = bvh8_code(bvh8_meta(m0, m1, key[0] & 7u), child_base, leaf_base);
+        continue;
+      }
+    } else {
+      const uint32_t count = (cur & 15u) + 1u;
+      F4 rec[4] = {v[0], v[1], v[2], v[3]};
+      for (uint32_t k = 0;;) {
+        float t, u, vv;
+        uint32_t ref;
+        if (hit_record<FT>(rec, o, d, time, tmin, tr.best.t, t, u, vv, ref)) {
+          tr.best.t = t;
+          tr.best.u = u;
+          tr.best.v = vv;
+          tr.best.ref = ref;
+        }
+        if (++k >= count) break;
+        const F4* q = sc.recs8 + 4 * (size_t)(first + k);
+        for (int e = 0; e < 4; ++e) rec[e] = ld_glb(q + e);
+      }
+    }
+    if (sp == 0) cur = TRAV_DONE;
+    else cur = stack.pop(--sp);
+  }
+  tr.cur = cur;
+  tr.sp = sp;
   return n;
 }
 
@@ -1123,6 +1246,19 @@ struct WStack {
       st_glb(P.stack + hbm_index(P, slot, k), v);
     }
   }
+  // entry k (the top) *= w: a dominated clamp vertex merged into it (shade_core)
+  RT_D void mul(const Params& P, uint32_t slot, uint32_t k, f3 w) const {
+    if ((int)k < nlds) {
+      lds_f32* q = (lds_f32*)lds + k * 256;
+      q[0] *= w.x;
+      q[nlds * 256] *= w.y;
+      q[2 * nlds * 256] *= w.z;
+    } else {
+      F4* e = P.stack + hbm_index(P, slot, k);
+      const F4 v = ld_glb(e);
+      st_glb(e, {v.x * w.x, v.y * w.y, v.z * w.z, 0.0f});
+    }
+  }
   // HBM entries: [entry][slot] (a wave's lanes at one depth coalesce) or, with
   // WSTACK_SLOT_MAJOR, [slot][entry] (one lane's pushes share cache lines)
   RT_D size_t hbm_index(const Params& P, uint32_t slot, uint32_t k) const {
@@ -1392,12 +1528,33 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
       // vertex bookkeeping (H1: the clamp is folded backwards at termination)
       if (clamp_vertex) {
         if (s.flags & F_PEND) {
-          f3 pv = get_pend<SOA>(P, slot, s);
-          ws.put(P, slot, s.nst, {pv.x, pv.y, pv.z, 0.0f});
-          ++s.nst;
-#ifdef RT_COUNT_PUSHES
-          ++s.pushes;  // a per-lane counter costs the fused kernels a VGPR: opt-in
+          const f3 pv = get_pend<SOA>(P, slot, s);
+#ifndef RT_NO_WEIGHT_MERGE
+          // Dominated clamp vertices are merged, not pushed.  The fold needs
+          // max_k I(P_k) over the suffix products P_k = w_k (.) P_k+1 (WStack::fold_max);
+          // with 0 <= w_k <= 1 in every channel, I(P_k) <= I(P_k+1) whatever follows,
+          // so vertex k never sets the scale and only its product matters: w_k is
+          // multiplied into the entry below instead of taking a stack entry (the
+          // bottom entry is still pushed: merging it into the camera-side prefix
+          // `pre`, which the book2 kernel keeps in scratch, cost more than it saved).
+          // Same folded value up to fp32 rounding; paths through the water orb and
+          // the fog (book2, up to 40 isotropic vertices) keep most of their stack in LDS.
+          const bool merge = s.nst > 0 && pv.x >= 0.0f && pv.y >= 0.0f && pv.z >= 0.0f &&
+                             pv.x <= 1.0f && pv.y <= 1.0f && pv.z <= 1.0f;
+#else
+          const bool merge = false;
 #endif
+          if (merge) {
+            ws.mul(P, slot, s.nst - 1, pv);
+          } else {
+            ws.put(P, slot, s.nst, {pv.x, pv.y, pv.z, 0.0f});
+            ++s.nst;
+#ifdef RT_COUNT_PUSHES
+            ++s.pushes;  // a per-lane counter costs the fused kernels a VGPR: opt-in
+#elif defined(RT_COUNT_HBM_PUSHES)
+            if ((int)s.nst > ws.nlds) ++s.pushes;  // pushes that went to HBM (debug builds)
+#endif
+          }
         }
         set_pend<SOA>(P, slot, s, weight);
         s.flags |= F_PEND;
@@ -1465,6 +1622,10 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
 // range over 8 partition counters measured 6-12 % slower (C2, 1 and 8 ranks).
 struct WaveBatch {
   uint32_t next, end;  // wave-uniform
+#ifdef RT_GRAB_PREFETCH
+  uint32_t pf;         // lane 0: start of the prefetched batch (returning atomic in flight)
+  bool pf_live;        // wave-uniform
+#endif
 };
 RT_D uint32_t grab_chunk(const Params& P, WaveBatch& b, bool need) {
   const unsigned long long m = __ballot(need);
@@ -1476,6 +1637,16 @@ RT_D uint32_t grab_chunk(const Params& P, WaveBatch& b, bool need) {
   if (n <= avail) {
     mine = b.next + r;
     b.next += n;
+#ifdef RT_GRAB_PREFETCH
+  } else if (b.pf_live && n - avail <= P.grab_min) {
+    // the batch prefetched by an earlier call: its atomic has had a refill's worth of
+    // work to return, so the read below rarely waits
+    const uint32_t g = __builtin_amdgcn_readlane(b.pf, 0);
+    b.pf_live = false;
+    mine = r < avail ? b.next + r : g + (r - avail);
+    b.next = g + (n - avail);
+    b.end = g + P.grab_min;
+#endif
   } else {
     // (smaller batches over the last part of the range measured 4-15 % slower,
     // even over its last 0.5 %: profiles/r1_wave_timeline.jsonl, r1_tail_sweep.jsonl)
@@ -1487,6 +1658,14 @@ RT_D uint32_t grab_chunk(const Params& P, WaveBatch& b, bool need) {
     b.next = g + (n - avail);
     b.end = g + grab;
   }
+#ifdef RT_GRAB_PREFETCH
+  // once the batch is half used, take the next one with a returning atomic whose
+  // result is read only at the next refill (lane 0 issues it; nothing waits here)
+  if (!b.pf_live && 2 * (b.end - b.next) < P.grab_min && b.end < P.n_chunks) {
+    if (lane_id() == 0) b.pf = atomicAdd(&P.ctr->chunk_head, P.grab_min);
+    b.pf_live = true;
+  }
+#endif
   if (!need) return 0xFFFFFFFFu;
   return mine < P.n_chunks ? mine : 0xFFFFFFFFu;
 }

@@ -28,6 +28,8 @@
 #include <thread>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "rt_internal.h"
 #include "rt_path.h"
 
@@ -57,6 +59,10 @@ RT_D void record_trace(const Params& P, const Path& s, const Hit& best) {
 // media + debug trace on top of the world closest hit, camera.go:300
 template <uint32_t FT>
 RT_D void finish_hit(const Params& P, const Path& s, Hit& best) {
+#ifndef RT_NO_TRI_REFINE
+  if (HAS(FT_TRI) && best.ref != PRIM_NONE && (best.ref >> 30) == PRIM_TRI)
+    refine_tri_hit(P.sc, best.ref & 0x3FFFFFFFu, s.o, s.d, best.t, best.u, best.v);
+#endif
 #ifdef ABL_NO_MEDIA
   if (false)
 #else
@@ -252,7 +258,7 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
   for (int ch = 0; ch < 3; ++ch) lacc[ch * 256 + threadIdx.x] = 0ull;
   if constexpr (HAS(FT_NOISE)) stage_perlin(P.sc);  // before stage_nodes' barrier
   if constexpr (cam_lds(FT)) stage_camera(P);
-  const bool recs_lds = LDS && stage_nodes(P, lnodes, TREE == 4 ? 8 : 4);
+  const bool recs_lds = LDS && TREE != 8 && stage_nodes(P, lnodes, TREE == 4 ? 8 : 4);
   if (!LDS) __syncthreads();  // staged tables visible to every wave (stage_nodes ends with one)
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;  // weight-stack column
   const TravStack ts = {&lstack[threadIdx.x], P.ostack + slot, P.stack_cols, fused_short(FT, TREE)};
@@ -268,7 +274,7 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
   Trav tr;
   tr.cur = TRAV_DONE;
   bool has = false;
-  WaveBatch b = {0u, 0u};
+  WaveBatch b = {};
   const unsigned long long t_start = P.wave_times ? wall_clock64() : 0ull;
   // Scheduling round: lanes without work take a chunk; traversing lanes run up
   // to step_budget traversal steps; lanes whose traversal is done are shaded
@@ -296,6 +302,14 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
       PH_CNT(PH_TRAV_ROUNDS, 1);
       if constexpr (TREE == 0)
         trav_brute<FT, !LDS>(P.sc, lnodes, s.o, s.d, s.time, 0.001f, tr);
+      else if constexpr (TREE == 8)
+      {
+        const int nsteps = trav_steps8<FT>(P.sc, ts, s.o, s.d, s.time, 0.001f, tr, P.step_budget);
+#ifdef RT_PHASES
+        ph_steps(nsteps);
+#endif
+        (void)nsteps;
+      }
       else
       {
         const int nsteps = trav_steps<LDS, FT, TREE == 4>(P.sc, lnodes, recs_lds, ts, s.o, s.d,
@@ -449,8 +463,37 @@ struct DeviceGuard {
   }
 };
 
+// rt_render_multi's RCCL gather (RT_FLAG_GATHER_RCCL): one communicator per device of
+// the list (ncclCommInitAll), a stream and a padded send buffer per share, kept while
+// the device list and the share size stay the same
+struct RcclGather {
+  std::vector<int> devs;
+  std::vector<ncclComm_t> comms;
+  std::vector<hipStream_t> streams;
+  std::vector<float*> send;
+  size_t send_floats = 0;
+  void release() {
+    for (size_t i = 0; i < comms.size(); ++i) {
+      (void)hipSetDevice(devs[i]);
+      if (send.size() > i && send[i]) (void)hipFree(send[i]);
+      if (streams.size() > i && streams[i]) (void)hipStreamDestroy(streams[i]);
+      (void)ncclCommDestroy(comms[i]);
+    }
+    devs.clear();
+    comms.clear();
+    streams.clear();
+    send.clear();
+    send_floats = 0;
+  }
+};
+
 void release_device(Scene* s) {
   DeviceGuard dg;
+  if (s->rccl) {
+    static_cast<RcclGather*>(s->rccl)->release();
+    delete static_cast<RcclGather*>(s->rccl);
+    s->rccl = nullptr;
+  }
   std::lock_guard<std::mutex> lk(s->mu);
   for (auto& kv : s->slots) {
     if (kv.second->st) {
@@ -492,6 +535,7 @@ static int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e && *e ? atoi(e) : dflt;
 }
+
 
 static FastDiv make_fastdiv(uint32_t d) {
   FastDiv f{1u, 0u, 0u, d};
@@ -629,8 +673,13 @@ static int upload_scene(const Scene* s, DeviceScene* ds) {
   {
     std::vector<F4> recs, lrecs;
     build_leaf_records(h, recs);
-    recs.resize(recs.size() + 4, F4{0, 0, 0, 0});  // trav_steps' 7-F4 fetch past the last record
     UP(recs, leafprims);
+    if (!h.refs8.empty()) {  // the BVH8's records, in its node order
+      std::vector<F4> r8(4 * h.refs8.size());
+      for (size_t i = 0; i < h.refs8.size(); ++i) make_record(h, h.refs8[i], &r8[4 * i]);
+      UP(r8, recs8);
+      UP(h.nodes8, nodes8);
+    }
     build_light_records(h, lrecs);
     UP(lrecs, light_recs);
     if (!small) goto records_done;
@@ -832,6 +881,12 @@ static const void* pick_fused(bool lds, uint32_t set, int tree) {
   if (tree == 0 && !lds && set == kFtSets[1]) return (const void*)k_fused<false, kFtSets[1], 0>;
   if (tree == 2 && lds && set == kFtSets[0]) return (const void*)k_fused<true, kFtSets[0], 2>;
   if (tree == 2 && lds && set == kFtSets[1]) return (const void*)k_fused<true, kFtSets[1], 2>;
+  if (tree == 8 && !lds) {  // BVH8: large trees read through L1/L2, the three tree sets
+    if (set == kFtSets[2]) return (const void*)k_fused<false, kFtSets[2], 8>;
+    if (set == kFtSets[3]) return (const void*)k_fused<false, kFtSets[3], 8>;
+    if (set == kFtSets[4]) return (const void*)k_fused<false, kFtSets[4], 8>;
+    return nullptr;
+  }
   if (tree != 4) return nullptr;  // no such kernel: render_impl never asks (see tree there)
   return lds ? fused_for<true>(set) : fused_for<false>(set);
 }
@@ -933,6 +988,11 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   const bool f_lds = node_slots * n_nodes <= lds_slots && !brute_smem;
   const size_t rec_slots = tree == 0 ? brute_slots : n_refs;
   const bool f_recs = f_lds && node_slots * n_nodes + rec_slots <= lds_slots;
+  // Trees read through L1/L2 take the BVH8 (host_bvh8.cpp) when the scene has one (built
+  // only with RT_BVH8=1) and a kernel exists for its feature set; RT_TREE=4 keeps the BVH4
+  if (mode == RT_MODE_FUSED && tree == 4 && !f_lds && !s->h.nodes8.empty() && env_tree != 4 &&
+      pick_fused(false, ft_set, 8))
+    tree = 8;
   const void* fused_kernel = pick_fused(f_lds, ft_set, tree);
   if (!fused_kernel) return set_error(RT_ERR_UNSUPPORTED, "internal: no fused kernel for this scene");
   const size_t fused_lds = f_lds ? 64 * (node_slots * n_nodes + (f_recs ? rec_slots : 0)) : 0;
@@ -1005,6 +1065,8 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     p.sc.nodes = ds->nodes2;
     p.sc.root = ds->root2;
     p.sc.n_nodes = ds->n_nodes2;
+  } else if (tree == 8) {
+    p.sc.root = 0;  // BVH8 node 0 (trav_init)
   } else if (tree == 0) {
     p.sc.n_nodes = 0;  // records only (stage_nodes puts them at the start of the cache)
     p.sc.leafprims = ds->brute_pairs;
@@ -1399,6 +1461,45 @@ static int render_multi(rt_scene* scene, const rt_camera* cam, const rt_render_o
       s->prog.busy = 1;
     }
   }
+  // RCCL gather (RT_FLAG_GATHER_RCCL): communicators over the device list, cached
+  const bool use_rccl = (o.flags & RT_FLAG_GATHER_RCCL) != 0;
+  RcclGather* rg = nullptr;
+  const size_t share_floats = (size_t)rows_per * W * 3;
+  if (use_rccl) {
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < i; ++j)
+        if (devices[i] == devices[j])
+          return set_error(RT_ERR_INVALID, "rt_render_multi: RCCL gather needs distinct devices");
+    if (!s->rccl) s->rccl = new RcclGather();
+    rg = static_cast<RcclGather*>(s->rccl);
+    if (rg->devs != std::vector<int>(devices, devices + n)) {
+      rg->release();
+      rg->devs.assign(devices, devices + n);
+      rg->comms.assign(n, nullptr);
+      const ncclResult_t r = ncclCommInitAll(rg->comms.data(), n, devices);
+      if (r != ncclSuccess) {
+        rg->comms.clear();
+        rg->devs.clear();
+        return set_error(RT_ERR_DEVICE, "rt_render_multi: ncclCommInitAll: %s", ncclGetErrorString(r));
+      }
+      rg->streams.assign(n, nullptr);
+      rg->send.assign(n, nullptr);
+      for (int i = 0; i < n; ++i) {
+        HIP_OK(hipSetDevice(devices[i]));
+        HIP_OK(hipStreamCreateWithFlags(&rg->streams[i], hipStreamNonBlocking));
+      }
+    }
+    if (rg->send_floats < share_floats) {
+      for (int i = 0; i < n; ++i) {
+        HIP_OK(hipSetDevice(devices[i]));
+        if (rg->send[i]) HIP_OK(hipFree(rg->send[i]));
+        rg->send[i] = nullptr;
+        HIP_OK(hipMalloc(&rg->send[i], std::max<size_t>(share_floats, 1) * sizeof(float)));
+      }
+      rg->send_floats = share_floats;
+    }
+    HIP_OK(hipSetDevice(d0));
+  }
   std::vector<rt_stats> st(n);
   std::vector<int> rcs(n, RT_OK);
   std::vector<std::string> errs(n);
@@ -1411,7 +1512,10 @@ static int render_multi(rt_scene* scene, const rt_camera* cam, const rt_render_o
       oi.nranks = n;
       oi.progress_slices = 0;
       const Gather g = {gbuf + (size_t)i * rows_per * W * 3, d0};
-      rcs[i] = render_impl(scene, cam, &oi, nullptr, nullptr, &st[i], 1 + i, &g);
+      if (rg)  // the share's rows into its padded send buffer; the gather follows
+        rcs[i] = render_impl(scene, cam, &oi, nullptr, rg->send[i], &st[i], 1 + i, nullptr);
+      else
+        rcs[i] = render_impl(scene, cam, &oi, nullptr, nullptr, &st[i], 1 + i, &g);
       if (rcs[i] != RT_OK) errs[i] = rt_last_error();
     });
   for (auto& t : th) t.join();
@@ -1428,6 +1532,24 @@ static int render_multi(rt_scene* scene, const rt_camera* cam, const rt_render_o
   } prog_done{s->prog, track};
   for (int i = 0; i < n; ++i)
     if (rcs[i] != RT_OK) return set_error(rcs[i], "rt_render_multi share %d: %s", i, errs[i].c_str());
+  if (rg && share_floats > 0) {
+    // one collective: every share's [rows_per][W][3] tile to devices[0]'s gather buffer
+    // (rank-major, the layout k_deinterleave reads); rows past a short share are padding
+    ncclResult_t r = ncclGroupStart();
+    for (int i = 0; r == ncclSuccess && i < n; ++i) {
+      HIP_OK(hipSetDevice(devices[i]));
+      r = ncclGather(rg->send[i], i == 0 ? (void*)gbuf : nullptr, share_floats, ncclFloat32, 0,
+                     rg->comms[i], rg->streams[i]);
+    }
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r == ncclSuccess) r = r2;
+    if (r != ncclSuccess)
+      return set_error(RT_ERR_DEVICE, "rt_render_multi: ncclGather: %s", ncclGetErrorString(r));
+    for (int i = 0; i < n; ++i) {
+      HIP_OK(hipSetDevice(devices[i]));
+      HIP_OK(hipStreamSynchronize(rg->streams[i]));
+    }
+  }
   HIP_OK(hipSetDevice(d0));
   if (img_floats > 0) {
     hipLaunchKernelGGL(k_deinterleave, dim3((unsigned)((img_floats + 255) / 256)), dim3(256), 0,

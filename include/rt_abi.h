@@ -297,10 +297,20 @@ int rt_scene_info_get(const rt_scene* s, rt_scene_info* out);
  * leaf child encoding documented in DESIGN.md.  Pass NULL to query counts. */
 int rt_scene_export_bvh(const rt_scene* s, float* nodes, int32_t* n_nodes, uint32_t* prim_refs,
                         int32_t* n_refs, uint32_t* root);
+/* the wide tree large scenes render with: BVH8 nodes as 32 floats
+ * (rt_device.h "BVH8 node", 16-bit planes) and the prim ref of each of its leaf
+ * records; 0 nodes when the scene has none.  Pass NULL to query counts. */
+int rt_scene_export_bvh8(const rt_scene* s, float* nodes, int32_t* n_nodes, uint32_t* refs8,
+                         int32_t* n_refs8);
 /* world-prim float AABBs in prim-ref order (6 floats each) */
 int rt_scene_export_prim_bounds(const rt_scene* s, float* bounds, int32_t* n);
 
-enum { RT_FLAG_PROFILE = 1 }; /* time every kernel with HIP events */
+enum {
+  RT_FLAG_PROFILE = 1,     /* time every kernel with HIP events */
+  RT_FLAG_GATHER_RCCL = 2  /* rt_render_multi: gather the shares with one RCCL ncclGather
+                              (communicators over the device list, cached per scene;
+                              the devices must be distinct) instead of peer copies */
+};
 
 /* execution strategy of the same per-vertex code (DESIGN.md "Kernels"):
  *   WAVEFRONT: queue-driven extend / shade kernels, path state in HBM (SoA)
@@ -385,6 +395,9 @@ int rt_render_device(rt_scene* s, const rt_camera* cam, const rt_render_opts* op
  * devices[0].  The image is bit-identical to rt_render's for any n (per-sample
  * fixed-point pixel sums).  opts->rank/nranks must be 0/1 and opts->stream NULL;
  * stats sum samples/segments over shares, ms_fused is the slowest share's.
+ * opts->flags & RT_FLAG_GATHER_RCCL: each share renders into a padded send buffer on
+ * its device and ONE ncclGather (RCCL over xGMI, root devices[0]) collects them, the
+ * survey's collective for this step; same image bits.
  * One rt_render_multi per scene at a time (a second call waits). */
 int rt_render_multi(rt_scene* s, const rt_camera* cam, const rt_render_opts* opts,
                     const int32_t* devices, int32_t n, float* out_rgb, rt_stats* stats);

@@ -8,8 +8,10 @@ import os
 import numpy as np
 
 
-def compare(gpu_img, ref_img):
-    """Per-pixel agreement statistics on linear RGB and on the 8-bit output."""
+def compare(gpu_img, ref_img, label=None):
+    """Per-pixel agreement statistics on linear RGB and on the 8-bit output.
+    `label` tags the PARITY_LOG line (e.g. "fp32_oracle" for the oracle's fp32 twin
+    against its fp64 path: what an fp32 evaluation of the reference itself reaches)."""
     import go_raytracer_amd as rt
     g = np.asarray(gpu_img, np.float64)
     r = np.asarray(ref_img, np.float64)
@@ -34,5 +36,6 @@ def compare(gpu_img, ref_img):
     if os.environ.get("PARITY_LOG"):
         with open(os.environ["PARITY_LOG"], "a") as f:
             f.write(json.dumps({"test": os.environ.get("PYTEST_CURRENT_TEST", ""),
+                                **({"label": label} if label else {}),
                                 **{k: float(v) for k, v in m.items()}}) + "\n")
     return m

@@ -54,3 +54,20 @@ def test_auto_builder_threshold(rt, gpu, monkeypatch):
     monkeypatch.setenv("RT_BVH_DEVICE_MIN", "100000")
     with rt.Scene(t, w, l) as sc:
         assert sc.info()["bvh_builder"] == 0
+
+
+@pytest.mark.parametrize("name,width,spp", [("model:256x32", 96, 16), ("book2", 64, 16)])
+def test_bvh8_renders_like_bvh4(rt, gpu, monkeypatch, name, width, spp):
+    """The opt-in BVH8 (RT_BVH8=1, host_bvh8.cpp, 16-bit planes) tests the same leaves
+    as the BVH4: the closest hit does not depend on the tree, so the image is the same
+    bits (conservative quantisation; ties between coincident surfaces aside)."""
+    imgs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("RT_BVH8", v)
+        t, cam, w, l = rt.demo_scene(name)
+        cam.Width, cam.SamplesPerPixel = width, spp
+        with rt.Scene(t, w, l) as sc:
+            img, st = sc.render(cam, seed=5, mode="fused")
+            assert st["tree_width"] == (8 if v == "1" else 4)
+        imgs.append(img)
+    assert np.array_equal(imgs[0], imgs[1], equal_nan=True)

@@ -24,7 +24,11 @@ def test_feature_parity(rt, oracle, gpu, name, mode):
         img, st = sc.render(cam, seed=11, mode=mode)
     ref, ost = oracle.render(t, w, l, cam, seed=11, threads=8)
     m = compare(img, ref)
-    print(name, mode, m, st["segments"], ost["segments"])
+    # the fp32 floor: the oracle's fp32 twin (the reference's algorithm in float)
+    # against its fp64 path, logged next to the GPU's numbers (PARITY_LOG)
+    ref32, _ = oracle.render(t, w, l, cam, seed=11, threads=8, precision=32)
+    m32 = compare(ref32, ref, label="fp32_oracle")
+    print(name, mode, m, m32, st["segments"], ost["segments"])
     assert st["samples"] == ost["samples"]
     assert abs(st["segments"] - ost["segments"]) <= 0.01 * ost["segments"] + 10
     assert m["frac_close"] >= 0.995, m

@@ -109,7 +109,11 @@ def test_full_size_parity_on_row_subsample(rt, oracle, gpu, name, width, spp, as
     assert np.isfinite(img).mean() > 0.999
     ref, ost = oracle.render(t, w, l, cam, seed=1, threads=16, rank=0, nranks=stride)
     m = compare(img[0::stride], ref)
-    print(name, m)
+    # the fp32 floor on the same rows (the oracle's fp32 twin vs its fp64 path)
+    ref32, _ = oracle.render(t, w, l, cam, seed=1, threads=16, rank=0, nranks=stride,
+                             precision=32)
+    m32 = compare(ref32, ref, label="fp32_oracle")
+    print(name, m, m32)
     assert m["frac_close"] >= bar and m["q_equal"] >= bar, m
     assert abs(m["mean_gpu"] - m["mean_ref"]) <= 2e-3 * max(1.0, abs(m["mean_ref"]))
     seg_ratio = (st["segments"] / st["samples"]) / (ost["segments"] / ost["samples"])
@@ -171,6 +175,29 @@ def test_render_multi_same_device_is_bitwise(rt, gpu):
     assert np.array_equal(one, again, equal_nan=True)
     assert stm["samples"] == st1["samples"] and stm["rows"] == one.shape[0]
     assert stm["segments"] == st1["segments"]
+
+
+def test_render_multi_rccl_gather(rt, gpu):
+    """RT_FLAG_GATHER_RCCL: the shares gathered by one ncclGather (communicators over the
+    device list) give the same bits as the peer-copy path and a one-device render.  On a
+    one-GPU box the list is [0] (RCCL needs distinct devices: [0, 0] is refused with an
+    error, not a crash); with two or more GPUs also [0, 1] and [1, 0]."""
+    t, cam, w, l = _scene(rt, "cornell", 97, 16)
+    cam.AspectRatio = 97 / 61
+    n = rt.device_count()
+    with rt.Scene(t, w, l) as sc:
+        one, st1 = sc.render(cam, seed=6)
+        a, sta = sc.render_multi(cam, [0], seed=6, rccl=True)
+        b, _ = sc.render_multi(cam, [0], seed=6, rccl=True)  # cached communicators
+        assert np.array_equal(one, a, equal_nan=True)
+        assert np.array_equal(one, b, equal_nan=True)
+        assert sta["samples"] == st1["samples"]
+        with pytest.raises(RuntimeError):
+            sc.render_multi(cam, [0, 0], seed=6, rccl=True)
+        if n >= 2:
+            for devs in ([0, 1], [1, 0]):
+                c, _ = sc.render_multi(cam, devs, seed=6, rccl=True)
+                assert np.array_equal(one, c, equal_nan=True), devs
 
 
 def test_render_multi_device_output(rt, gpu):

@@ -87,6 +87,69 @@ def test_bvh_invariants(rt, name):
         bvh_invariants(sc)
 
 
+def bvh8_invariants(sc):
+    """host_bvh8.cpp: every world prim has exactly one BVH8 leaf record, every node is
+    reached once through child_base + rank, and every child box dequantised with the
+    device's fp32 arithmetic (origin + q * 2^(E-127)) contains what is below it."""
+    nodes, refs8 = sc.export_bvh8()
+    _, refs, _, bounds = sc.export_bvh()
+    assert len(nodes) > 0
+    assert sorted(refs8.tolist()) == sorted(refs.tolist())
+    bound_of = {int(r): bounds[i] for i, r in enumerate(refs)}
+    visits = np.zeros(len(nodes), np.int32)
+    f32 = np.float32
+    stack = [(0, np.full(3, -np.inf, f32), np.full(3, np.inf, f32))]
+    while stack:
+        ni, plo, phi = stack.pop()
+        visits[ni] += 1
+        w = nodes[ni]
+        origin = w[0:3].view(np.float32)
+        ex = [(int(w[3]) >> (8 * a)) & 0xFF for a in range(3)]
+        scale = np.array([np.uint32(e << 23) for e in ex], np.uint32).view(np.float32)
+        child_base, leaf_base = int(w[4]), int(w[5])
+        meta = [(int(w[6 + k // 4]) >> (8 * (k % 4))) & 0xFF for k in range(8)]
+        q = np.zeros((6, 8), np.uint32)
+        for f in range(6):
+            for k in range(8):
+                word = int(w[8 + 4 * f + k // 2])
+                q[f, k] = (word >> (16 * (k & 1))) & 0xFFFF
+        for k, m in enumerate(meta):
+            if m == 0xFF:
+                continue
+            lo = np.array([f32(origin[a]) + f32(q[2 * a, k]) * scale[a] for a in range(3)], f32)
+            hi = np.array([f32(origin[a]) + f32(q[2 * a + 1, k]) * scale[a] for a in range(3)], f32)
+            assert (lo <= hi).all()
+            if m & 0x80:
+                stack.append((child_base + (m & 7), np.maximum(lo, plo), np.minimum(hi, phi)))
+            else:
+                first, cnt = leaf_base + (m & 31), ((m >> 5) & 3) + 1
+                for r in refs8[first:first + cnt]:
+                    b = bound_of[int(r)]
+                    assert (b[:3] >= lo).all() and (b[3:] <= hi).all()
+                    assert (b[:3] >= plo).all() and (b[3:] <= phi).all()
+    assert (visits == 1).all(), "every BVH8 node is reached exactly once"
+    return nodes, refs8
+
+
+@pytest.mark.parametrize("name", ["book2", "model:96x24"])
+def test_bvh8_invariants(rt, name, monkeypatch):
+    monkeypatch.setenv("RT_BVH8", "1")  # the wide tree is opt-in (DESIGN.md §9)
+    t, cam, w, l = rt.demo_scene(name)
+    with rt.Scene(t, w, l) as sc:
+        nodes, _ = bvh8_invariants(sc)
+    assert len(nodes) >= 2
+
+
+def test_bvh8_only_when_asked_and_large(rt, monkeypatch):
+    t, cam, w, l = rt.demo_scene("book2")
+    with rt.Scene(t, w, l) as sc:  # default: no BVH8
+        assert len(sc.export_bvh8()[0]) == 0
+    monkeypatch.setenv("RT_BVH8", "1")
+    t, cam, w, l = rt.demo_scene("book1")  # 485 prims: the BVH4 (LDS-sized scenes)
+    with rt.Scene(t, w, l) as sc:
+        assert len(sc.export_bvh8()[0]) == 0
+
+
 def test_light_table_matches_nested_picks(rt):
     """lights = list(list(a, b), c): the flattened pick intervals must select
     exactly what nested rand.Intn picks select (hittable.go:98-103)."""
