@@ -29,8 +29,12 @@ RT_D float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 RT_D f3 cross(f3 a, f3 b) {
   return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
 }
-RT_D float length(f3 a) { return sqrtf(dot(a, a)); }
-// v_rcp_f32 (1 ulp): no range-scaling fix-up sequence around the reciprocal
+// v_sqrt_f32 / v_rcp_f32 (1 ulp): without the denormal-range scaling (sqrtf emits
+// ldexp / cndmask around v_sqrt, and a correctly rounded sequence of ~14 ops in some
+// contexts).  Arguments here are lengths and [0,1] sampling values; a denormal one
+// is off by less than its own size.
+RT_D float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+RT_D float length(f3 a) { return fsqrt(dot(a, a)); }
 RT_D float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 RT_D f3 unit(f3 a) { return a * rcp(length(a)); }  // UnitVector vec.go:125
 RT_D bool finite3(f3 a) { return isfinite(a.x) && isfinite(a.y) && isfinite(a.z); }
@@ -49,18 +53,18 @@ RT_D float sin2pi(float u) { return __builtin_amdgcn_sinf(u); }
 // RandomUnitVector vec.go:159-167 (uniform on the sphere)
 RT_D f3 uniform_sphere(float u0, float u1) {
   float z = 1.0f - 2.0f * u0;
-  float r = sqrtf(fmaxf(0.0f, 1.0f - z * z));
+  float r = fsqrt(fmaxf(0.0f, 1.0f - z * z));
   return {r * cos2pi(u1), r * sin2pi(u1), z};
 }
 // RandomUnitDisk vec.go:149-156 (uniform in the disk)
 RT_D f3 uniform_disk(float u0, float u1) {
-  float r = sqrtf(u0);
+  float r = fsqrt(u0);
   return {r * cos2pi(u1), r * sin2pi(u1), 0.0f};
 }
 // RandomCosineDirection vec.go:177-186: phi = 2*pi*r1
 RT_D f3 cosine_direction(float r1, float r2) {
-  float s = sqrtf(r2);
-  return {cos2pi(r1) * s, sin2pi(r1) * s, sqrtf(1.0f - r2)};
+  float s = fsqrt(r2);
+  return {cos2pi(r1) * s, sin2pi(r1) * s, fsqrt(1.0f - r2)};
 }
 
 // NewONB onb.go:13-25 — note the 0.9 test is on the un-normalised vector
@@ -82,7 +86,7 @@ RT_D f3 reflect(f3 v, f3 n) { return v - n * (dot(n, v) * 2.0f); }
 RT_D f3 refract(f3 v, f3 n, float eta) {
   float c = fminf(dot(-v, n), 1.0f);
   f3 perp = (v + n * c) * eta;
-  f3 par = n * (-sqrtf(fabsf(1.0f - dot(perp, perp))));
+  f3 par = n * (-fsqrt(fabsf(1.0f - dot(perp, perp))));
   return perp + par;
 }
 
@@ -280,7 +284,10 @@ RT_D bool hit_quad_rec(const F4 r[4], f3 o, f3 d, float tmin, float tmax, float&
   f3 pp = (o + d * t) - xyz(Q);
   float alpha = dot(pp, xyz(A));
   float beta = dot(pp, xyz(B));
-  if (!(0.0f <= alpha && alpha <= 1.0f) || !(0.0f <= beta && beta <= 1.0f)) return false;
+  // 0 <= alpha, beta <= 1 as one unsigned max + compare (non-negative floats order like
+  // their bits; negatives and NaN exceed 1.0f's bits; -0.0f is rejected where the
+  // reference accepts it: an exactly-zero coordinate of negative sign, measure zero)
+  if (max(__float_as_uint(alpha), __float_as_uint(beta)) > 0x3F800000u) return false;
   t_out = t;
   a_out = alpha;
   b_out = beta;

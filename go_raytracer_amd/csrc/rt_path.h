@@ -1027,8 +1027,8 @@ RT_D float prim_pdf(const DevScene& sc, uint32_t ref, int li, f3 origin, f3 dir)
     const F4 cr = sc.sph_cr[idx];
     f3 oc = xyz(cr) - origin;
     float dist2 = dot(oc, oc);
-    float cmax = sqrtf(1.0f - cr.w * cr.w / dist2);
-    return 1.0f / (2.0f * kPi * (1.0f - cmax));
+    float cmax = fsqrt(1.0f - cr.w * cr.w * rcp(dist2));
+    return rcp(2.0f * kPi * (1.0f - cmax));
   }
   float t, u, v, area;
   f3 n;
@@ -1050,9 +1050,9 @@ RT_D float prim_pdf(const DevScene& sc, uint32_t ref, int li, f3 origin, f3 dir)
     n = tri_normal(sc, idx, u, v);
     area = sc.tri[3 * (size_t)idx + 1].w;
   }
-  float dist2 = t * t * dot(dir, dir);
-  float cosine = fabsf(dot(dir, n) / length(dir));
-  return dist2 / (cosine * area);
+  // dist2 / (cosine * area) with dist2 = t^2 |dir|^2, cosine = |dir.n| / |dir|
+  const float dd = dot(dir, dir);
+  return (t * t * dd) * fsqrt(dd) * rcp(fabsf(dot(dir, n)) * area);
 }
 
 // HittableList.PdfValue hittable.go:89-97 over the flattened light table
@@ -1090,8 +1090,8 @@ RT_D f3 lights_random(const DevScene& sc, f3 origin, const rt_u32x4& r) {
     f3 dir = xyz(cr) - origin;
     float dist2 = dot(dir, dir);
     Onb b = make_onb(dir);
-    float z = 1.0f + s1 * (sqrtf(1.0f - cr.w * cr.w / dist2) - 1.0f);
-    float tt = sqrtf(1.0f - z * z);  // phi = 2*pi*s0
+    float z = 1.0f + s1 * (fsqrt(1.0f - cr.w * cr.w * rcp(dist2)) - 1.0f);
+    float tt = fsqrt(1.0f - z * z);  // phi = 2*pi*s0
     return onb_transform(b, mk3(cos2pi(s0) * tt, sin2pi(s0) * tt, z));
   }
   if (!HAS(FT_TRI) || type == PRIM_QUAD) {  // quad.Random objects.go:161-165
@@ -1246,18 +1246,23 @@ struct WStack {
       st_glb(P.stack + hbm_index(P, slot, k), v);
     }
   }
-  // entry k (the top) *= w: a dominated clamp vertex merged into it (shade_core)
-  RT_D void mul(const Params& P, uint32_t slot, uint32_t k, f3 w) const {
+  // entry k (the top) *= w: a dominated clamp vertex merged into it (shade_core);
+  // returns the new entry
+  RT_D f3 mul(const Params& P, uint32_t slot, uint32_t k, f3 w) const {
+    f3 r;
     if ((int)k < nlds) {
       lds_f32* q = (lds_f32*)lds + k * 256;
-      q[0] *= w.x;
-      q[nlds * 256] *= w.y;
-      q[2 * nlds * 256] *= w.z;
+      r = mk3(q[0] * w.x, q[nlds * 256] * w.y, q[2 * nlds * 256] * w.z);
+      q[0] = r.x;
+      q[nlds * 256] = r.y;
+      q[2 * nlds * 256] = r.z;
     } else {
       F4* e = P.stack + hbm_index(P, slot, k);
       const F4 v = ld_glb(e);
-      st_glb(e, {v.x * w.x, v.y * w.y, v.z * w.z, 0.0f});
+      r = mk3(v.x * w.x, v.y * w.y, v.z * w.z);
+      st_glb(e, {r.x, r.y, r.z, 0.0f});
     }
+    return r;
   }
   // HBM entries: [entry][slot] (a wave's lanes at one depth coalesce) or, with
   // WSTACK_SLOT_MAJOR, [slot][entry] (one lane's pushes share cache lines)
@@ -1279,7 +1284,19 @@ struct WStack {
   // `v` is pend (.) L with maxI = I(v) on entry; entries nst-1 .. 0: HBM ones (rare)
   // one by one, then the LDS ones, unrolled.
   RT_D void fold_max(const Params& P, uint32_t slot, uint32_t nst, f3& v, float& maxI) const {
-    for (int k = (int)nst - 1; k >= nlds; --k) {
+    int k = (int)nst - 1;
+#ifndef RT_FOLD_ONE_LOAD
+    // HBM entries two at a time: both loads in flight before the products need them
+    for (; k - 1 >= nlds; k -= 2) {
+      const F4 a = ld_glb(P.stack + hbm_index(P, slot, (uint32_t)k));
+      const F4 b = ld_glb(P.stack + hbm_index(P, slot, (uint32_t)(k - 1)));
+      v = xyz(a) * v;
+      maxI = fmaxf(maxI, v.x + v.y + v.z);
+      v = xyz(b) * v;
+      maxI = fmaxf(maxI, v.x + v.y + v.z);
+    }
+#endif
+    for (; k >= nlds; --k) {
       v = xyz(ld_glb(P.stack + hbm_index(P, slot, (uint32_t)k))) * v;
       maxI = fmaxf(maxI, v.x + v.y + v.z);
     }
@@ -1404,7 +1421,7 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
     if (HAS(FT_SPHERE) && type == PRIM_SPHERE) {
       const F4 cr = sc.sph_cr[idx], mv = sc.sph_mv[idx];
       f3 cc = xyz(cr) + xyz(mv) * time;
-      nout = (p - cc) * (1.0f / cr.w);
+      nout = (p - cc) * rcp(cr.w);
       mat = (int)fbits(mv.w);
       ff = dot(d, nout) < 0;  // setFaceNormal hittable.go:27-34
       n = ff ? nout : -nout;
@@ -1413,8 +1430,8 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
         f3 no = mk3(rs.x * nout.x - rs.y * nout.z, nout.y, rs.y * nout.x + rs.x * nout.z);
         float theta = acosf(-no.y);
         float phi = atan2f(-no.z, no.x) + kPi;
-        u = phi / (2.0f * kPi);
-        v = theta / kPi;
+        u = phi * (0.5f * kInvPi);
+        v = theta * kInvPi;
       }
     } else if (!HAS(FT_TRI | FT_MEDIA) || type == PRIM_QUAD) {
       const F4* q = sc.quad + 5 * (size_t)idx;
@@ -1477,14 +1494,14 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
         weight = xyz(M.albedo);
       } else if (HAS(FT_DIEL) && M.kind == RT_MAT_DIELECTRIC) {  // materials.go:94-130
         float ior = M.param;
-        float ri = ff ? 1.0f / ior : ior;
+        float ri = ff ? rcp(ior) : ior;
         f3 ud = unit(d);
         float cs = fminf(dot(-ud, n), 1.0f);
-        float sn = sqrtf(1.0f - cs * cs);
+        float sn = fsqrt(1.0f - cs * cs);
         bool cannot = ri * sn > 1.0f;
         bool refl = cannot;
         if (!cannot) {
-          float r0 = (1.0f - ior) / (1.0f + ior);
+          float r0 = (1.0f - ior) * rcp(1.0f + ior);
           r0 = r0 * r0;
           float refl_p = r0 + (1.0f - r0) * powf(1.0f - cs, 5.0f);
           refl = refl_p > rt_unit_f(r.v[0]);
@@ -1545,7 +1562,19 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
           const bool merge = false;
 #endif
           if (merge) {
-            ws.mul(P, slot, s.nst - 1, pv);
+            f3 top = ws.mul(P, slot, s.nst - 1, pv);
+            // Kernels with media also cascade: the merged top may itself now be
+            // dominated by the new clamp vertex (0 <= top <= 1), so it folds into the
+            // entry below, and so on.  Book2's HBM pushes: 309 M -> 126 M (merge) ->
+            // 19 M (cascade) at 400 x 400 x 1024; C4 -1.7 %, while the lean and mesh
+            // kernels, whose stacks stay shallow, lost 0.6-1.4 % to the loop
+            // (profiles/r3_weight_cascade_ab.jsonl).
+            if (HAS(FT_MEDIA))
+              while (s.nst >= 2 && top.x >= 0.0f && top.y >= 0.0f && top.z >= 0.0f &&
+                     top.x <= 1.0f && top.y <= 1.0f && top.z <= 1.0f) {
+                top = ws.mul(P, slot, s.nst - 2, top);
+                --s.nst;
+              }
           } else {
             ws.put(P, slot, s.nst, {pv.x, pv.y, pv.z, 0.0f});
             ++s.nst;
@@ -1622,10 +1651,6 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
 // range over 8 partition counters measured 6-12 % slower (C2, 1 and 8 ranks).
 struct WaveBatch {
   uint32_t next, end;  // wave-uniform
-#ifdef RT_GRAB_PREFETCH
-  uint32_t pf;         // lane 0: start of the prefetched batch (returning atomic in flight)
-  bool pf_live;        // wave-uniform
-#endif
 };
 RT_D uint32_t grab_chunk(const Params& P, WaveBatch& b, bool need) {
   const unsigned long long m = __ballot(need);
@@ -1637,16 +1662,6 @@ RT_D uint32_t grab_chunk(const Params& P, WaveBatch& b, bool need) {
   if (n <= avail) {
     mine = b.next + r;
     b.next += n;
-#ifdef RT_GRAB_PREFETCH
-  } else if (b.pf_live && n - avail <= P.grab_min) {
-    // the batch prefetched by an earlier call: its atomic has had a refill's worth of
-    // work to return, so the read below rarely waits
-    const uint32_t g = __builtin_amdgcn_readlane(b.pf, 0);
-    b.pf_live = false;
-    mine = r < avail ? b.next + r : g + (r - avail);
-    b.next = g + (n - avail);
-    b.end = g + P.grab_min;
-#endif
   } else {
     // (smaller batches over the last part of the range measured 4-15 % slower,
     // even over its last 0.5 %: profiles/r1_wave_timeline.jsonl, r1_tail_sweep.jsonl)
@@ -1658,14 +1673,6 @@ RT_D uint32_t grab_chunk(const Params& P, WaveBatch& b, bool need) {
     b.next = g + (n - avail);
     b.end = g + grab;
   }
-#ifdef RT_GRAB_PREFETCH
-  // once the batch is half used, take the next one with a returning atomic whose
-  // result is read only at the next refill (lane 0 issues it; nothing waits here)
-  if (!b.pf_live && 2 * (b.end - b.next) < P.grab_min && b.end < P.n_chunks) {
-    if (lane_id() == 0) b.pf = atomicAdd(&P.ctr->chunk_head, P.grab_min);
-    b.pf_live = true;
-  }
-#endif
   if (!need) return 0xFFFFFFFFu;
   return mine < P.n_chunks ? mine : 0xFFFFFFFFu;
 }

@@ -84,7 +84,14 @@ RT_RNG_FN rt_u32x4 rt_philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint3
 
 /* Four raw 32-bit draws for (pixel, sample, stream). */
 RT_RNG_FN rt_u32x4 rt_rng_draw(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t stream) {
-  return rt_philox4x32_10(pixel, sample, stream, 0u, (uint32_t)seed, (uint32_t)(seed >> 32));
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#if defined(__HIP_DEVICE_COMPILE__) && defined(RT_RNG_KEY_BARRIER)
+  /* (A/B builds) an empty asm that "changes" the key: the compiler cannot hoist the 18
+     round keys out of the kernels' main loops, where they sit in SGPRs for the whole
+     kernel; recomputing them is 18 scalar adds a call */
+  __asm__ volatile("" : "+s"(k0), "+s"(k1));
+#endif
+  return rt_philox4x32_10(pixel, sample, stream, 0u, k0, k1);
 }
 
 RT_RNG_FN uint32_t rt_u24(uint32_t x) { return x >> 8; }

@@ -39,3 +39,14 @@ def compare(gpu_img, ref_img, label=None):
                                 **({"label": label} if label else {}),
                                 **{k: float(v) for k, v in m.items()}}) + "\n")
     return m
+
+
+def fp32_bar(m32, key, bar=0.995, floor=0.99):
+    """The parity bar for metric `key` given the oracle's fp32 twin's agreement m32 with
+    its fp64 path (same scene, seed and pixels): SURVEY.md §8(c) P1's `bar` where an fp32
+    evaluation of the reference's own algorithm reaches it; otherwise the GPU must be at
+    least as close to fp64 as that fp32 evaluation, and never below `floor`.  (The north
+    star asks for agreement "within a stated fp32 tolerance"; on scenes whose paths are
+    chaotic -- C5's chains of metal bounces, a cluster of 200 small spheres -- fp32 and
+    fp64 paths fork after a few bounces whatever the implementation: tools/fork_probe.py.)"""
+    return bar if m32[key] >= bar else max(floor, m32[key])

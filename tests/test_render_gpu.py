@@ -5,7 +5,7 @@ fixed point), and oracle parity at BASELINE.json's full sizes on a row subsample
 import numpy as np
 import pytest
 
-from tests.parity import compare
+from tests.parity import compare, fp32_bar
 
 pytestmark = pytest.mark.gpu
 
@@ -88,19 +88,22 @@ def test_sample_overflow_is_flagged_not_clamped(rt, oracle, gpu):
 
 FULL = [
     # BASELINE.json configs at full size; the oracle checks every `stride`-th row.
-    # Bar: SURVEY.md §8(c) P1, >= 99.5 % of channels within 2^-10 and 8-bit equal,
-    # except C5: its 1M-triangle mesh puts many silhouette and shared-edge hits
-    # where fp32 and fp64 Moller-Trumbore disagree, each flipping a whole sample
-    # (calibrated: measured 99.26 % / 99.04 %, so the bar there is 99 %).
-    ("cornell", 800, 1024, 1.0, 100, 0.995),   # C2
-    ("book1", 1200, 512, 1.5, 160, 0.995),     # C3 (aspect 1.5 -> 800 rows, 484 spp)
-    ("book2", 800, 4096, 1.0, 100, 0.995),     # C4 (one GPU here; the split is rank-invariant)
-    ("model", 1920, 1024, 16 / 9, 216, 0.99),  # C5 (1M-triangle substitute mesh, 1920x1080)
+    # Bar: SURVEY.md §8(c) P1, >= 99.5 % of channels within 2^-10 and 8-bit equal, or --
+    # where the oracle's fp32 twin itself stays below that against its fp64 path on the
+    # same rows -- at least the fp32 twin's agreement and >= 99 % (tests/parity.py
+    # fp32_bar).  Only C5 takes the second form: its paths bounce along the metal knot
+    # and fork between fp32 and fp64 after 2-14 bounces of accumulated rounding
+    # (tools/fork_probe.py, profiles/r3_fork_probe_model_*.jsonl); measured GPU 0.9926 /
+    # fp32 twin 0.9849 (8-bit), profiles/r3_parity_v1.jsonl.
+    ("cornell", 800, 1024, 1.0, 100),   # C2
+    ("book1", 1200, 512, 1.5, 160),     # C3 (aspect 1.5 -> 800 rows, 484 spp)
+    ("book2", 800, 4096, 1.0, 100),     # C4 (one GPU here; the split is rank-invariant)
+    ("model", 1920, 1024, 16 / 9, 216),  # C5 (1M-triangle substitute mesh, 1920x1080)
 ]
 
 
-@pytest.mark.parametrize("name,width,spp,aspect,stride,bar", FULL)
-def test_full_size_parity_on_row_subsample(rt, oracle, gpu, name, width, spp, aspect, stride, bar):
+@pytest.mark.parametrize("name,width,spp,aspect,stride", FULL)
+def test_full_size_parity_on_row_subsample(rt, oracle, gpu, name, width, spp, aspect, stride):
     t, cam, w, l = _scene(rt, name, width, spp)
     cam.AspectRatio = aspect
     with rt.Scene(t, w, l) as sc:
@@ -114,7 +117,8 @@ def test_full_size_parity_on_row_subsample(rt, oracle, gpu, name, width, spp, as
                              precision=32)
     m32 = compare(ref32, ref, label="fp32_oracle")
     print(name, m, m32)
-    assert m["frac_close"] >= bar and m["q_equal"] >= bar, m
+    assert m["frac_close"] >= fp32_bar(m32, "frac_close"), (m, m32)
+    assert m["q_equal"] >= fp32_bar(m32, "q_equal"), (m, m32)
     assert abs(m["mean_gpu"] - m["mean_ref"]) <= 2e-3 * max(1.0, abs(m["mean_ref"]))
     seg_ratio = (st["segments"] / st["samples"]) / (ost["segments"] / ost["samples"])
     assert abs(seg_ratio - 1) < 0.01
