@@ -54,8 +54,8 @@ EXTRA = [("C3", "book1", 1200, 512, 3),   # main.go:19-91, aspect 1.5 -> 1200x80
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # 64 steps of C2: a ~3 s timed region (the driver samples GPU activity during it)
-    ap.add_argument("--steps", type=int, default=64)
+    # 128 steps of C2: a ~5.4 s timed region (the driver samples GPU activity during it)
+    ap.add_argument("--steps", type=int, default=128)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--scene", default="cornell")
     ap.add_argument("--width", type=int, default=800)
@@ -64,11 +64,14 @@ def parse():
     ap.add_argument("--mode", default="auto", choices=["auto", "fused", "wavefront"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra-configs", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline work")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline work")
     ap.add_argument("--devices", default=None,
                     help="single-process multi-GPU: comma-separated HIP devices rendered through "
                          "rt_render_multi (rows r on devices[r %% n], peer-gathered to devices[0]); "
                          "the north_star's Go-host path, no torchrun")
+    ap.add_argument("--gather", default="peer", choices=["peer", "rccl"],
+                    help="--devices mode: collect the shares on devices[0] by peer copies or by "
+                         "one RCCL ncclGather (RT_FLAG_GATHER_RCCL; distinct devices)")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"),
                     help="PMC counters per launch (tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -218,7 +221,8 @@ def main():
         def step(prof):
             if devices:  # one process: every share on its device, gathered on devices[0]
                 return scene.render_multi_device(cam, devices, buf.data_ptr(), seed=args.seed,
-                                                 profile=prof, mode=args.mode)
+                                                 profile=prof, mode=args.mode,
+                                                 rccl=args.gather == "rccl")
             st = scene.render_device(cam, buf.data_ptr(), seed=args.seed, device=local_rank,
                                      rank=rank, nranks=world_size, profile=prof,
                                      stream=stream.cuda_stream, mode=args.mode)
@@ -321,7 +325,9 @@ def main():
                        "scene": args.scene, "width": W, "height": H, "spp": d.spp_sqrt ** 2,
                        "max_depth": d.max_depth,
                        "parallelism": (f"rows%{len(devices)} in one process (rt_render_multi, "
-                                       f"devices {devices})") if devices else f"rows%{world_size}",
+                                       f"devices {devices}, {args.gather} gather)") if devices
+                                      else f"rows%{world_size} (RCCL gather to rank 0)"
+                                      if world_size > 1 else "rows%1",
                        "mode": mode, "path_slots": stats[0]["path_slots"],
                        "chunk_samples": stats[0]["chunk_samples"],
                        "segments_per_sample": round(seg / max(smp, 1), 4),

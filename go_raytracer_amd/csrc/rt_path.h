@@ -847,8 +847,35 @@ RT_D void trace_media(const Params& P, f3 o, f3 d, float time, float tmin, uint3
   const DevScene& sc = P.sc;
   rt_u32x4 r = {{0, 0, 0, 0}};
   int cached_group = -1;
+  const float ray_len = length(d);
   for (int mi = 0; mi < sc.n_media; ++mi) {
     const DevMedium m = sc.media[mi];
+    // The free-flight distance first (its draws are a pure function of the path's
+    // counters, rt_rng.h, so drawing them before the boundary test changes nothing).
+    // The medium's hit lies at max(t1, tmin) + hd / |d| > hd / |d|: when that is already
+    // past the closest hit, the medium cannot be the closest hit and its fp64 boundary
+    // roots are not needed -- book2's R = 5000 fog (mean free path 10^4) skips them on
+    // most segments.  Same result as computing them (tm < best.t fails either way).
+    float hd = kInf;
+    for (int k = 0; k < m.mult; ++k) {
+      int draw = m.draw_base + k;
+      float u;
+      if (draw == sc.medium_draws - 1) {
+        u = rt_unit_f(spare);
+      } else {
+        int group = 1 + (draw >> 2);
+        if (group != cached_group) {
+          r = rt_rng_draw(P.seed, gpix, sample, RT_STREAM(vertex, group));
+          cached_group = group;
+        }
+        u = rt_unit_f(r.v[draw & 3]);
+      }
+      hd = fminf(hd, m.neg_inv_density * logf(u));
+    }
+    const float hd_t = hd / ray_len;  // the same quotient as tm's below
+#ifndef RT_NO_MEDIA_SKIP
+    if (!(hd_t < best.t)) continue;
+#endif
     double t1, t2;
     const uint32_t b0 = m.bcount == 1 ? sc.medium_refs[m.bfirst] : PRIM_NONE;
     if ((b0 >> 30) == PRIM_SPHERE && b0 != PRIM_NONE) {
@@ -867,26 +894,9 @@ RT_D void trace_media(const Params& P, f3 o, f3 d, float time, float tmin, uint3
     t1 = fmax(t1, (double)tmin);
     if (t1 >= t2) continue;
     t1 = fmax(0.0, t1);
-    float ray_len = length(d);
     double inside = (t2 - t1) * (double)ray_len;
-    float hd = kInf;
-    for (int k = 0; k < m.mult; ++k) {
-      int draw = m.draw_base + k;
-      float u;
-      if (draw == sc.medium_draws - 1) {
-        u = rt_unit_f(spare);
-      } else {
-        int group = 1 + (draw >> 2);
-        if (group != cached_group) {
-          r = rt_rng_draw(P.seed, gpix, sample, RT_STREAM(vertex, group));
-          cached_group = group;
-        }
-        u = rt_unit_f(r.v[draw & 3]);
-      }
-      hd = fminf(hd, m.neg_inv_density * logf(u));
-    }
     if ((double)hd > inside) continue;
-    float tm = (float)(t1 + (double)(hd / ray_len));
+    float tm = (float)(t1 + (double)hd_t);
     if (tm < best.t) {
       best.t = tm;
       best.u = 0.0f;

@@ -225,10 +225,14 @@ constexpr int fused_waves(uint32_t ft, int tree = 4) {
 #ifndef ALL_WLDS
 #define ALL_WLDS 4  // 6 pushed the C3-size trees out of the 3-wave LDS budget
 #endif
+#ifndef BRUTE_WLDS
+#define BRUTE_WLDS kLdsWMax
+#endif
 constexpr int fused_wlds(uint32_t ft, int tree = 4) {
   return (ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ||
           ft == (FT_SPHERE | FT_TRI | FT_METAL)) ? MESH_WLDS
          : (ft == 0u && tree != 0)                                  ? 4
+         : (ft == 0u && tree == 0)                                  ? BRUTE_WLDS
          : ft == FT_ALL                                             ? ALL_WLDS
          : ft == (FT_SPHERE | FT_METAL | FT_DIEL | FT_MEDIA | FT_IMAGE | FT_NOISE) ? TEX_WLDS
                                                                     : kLdsWMax;

@@ -85,10 +85,11 @@ RT_RNG_FN rt_u32x4 rt_philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint3
 /* Four raw 32-bit draws for (pixel, sample, stream). */
 RT_RNG_FN rt_u32x4 rt_rng_draw(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t stream) {
   uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-#if defined(__HIP_DEVICE_COMPILE__) && defined(RT_RNG_KEY_BARRIER)
-  /* (A/B builds) an empty asm that "changes" the key: the compiler cannot hoist the 18
-     round keys out of the kernels' main loops, where they sit in SGPRs for the whole
-     kernel; recomputing them is 18 scalar adds a call */
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(RT_RNG_HOIST_KEYS)
+  /* an empty asm that "changes" the key: the compiler cannot hoist the 18 round keys out
+     of the fused kernels' main loops, where they sat in SGPRs for the whole kernel and
+     pushed other values out to VGPR lanes; recomputing them is 18 scalar adds a call
+     (C2 -1.5 %, C3 -0.7 %, C4 -0.5 %: profiles/r3_rng_keys_ab.jsonl) */
   __asm__ volatile("" : "+s"(k0), "+s"(k1));
 #endif
   return rt_philox4x32_10(pixel, sample, stream, 0u, k0, k1);

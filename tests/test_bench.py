@@ -36,3 +36,19 @@ def test_devices_mode_line(gpu):
     assert "rt_render_multi" in line["config"]["parallelism"]
     assert line["value"] > 0 and line["steps"] == 2
     assert line["roofline"]["launches"] == 2
+
+
+@pytest.mark.gpu
+def test_devices_mode_rccl_gather_line(gpu):
+    """--gather rccl: the shares collected by one ncclGather (RT_FLAG_GATHER_RCCL); on a
+    one-GPU box the device list is [0] (RCCL needs distinct devices)."""
+    p = _bench("--gpus", "1", "--devices", "0", "--gather", "rccl")
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert "rccl gather" in line["config"]["parallelism"]
+    assert line["value"] > 0 and line["steps"] == 2
+
+
+def test_gather_option_rejects_unknown():
+    p = _bench("--gather", "nccl-allgather")
+    assert p.returncode != 0 and "invalid choice" in p.stderr
