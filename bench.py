@@ -173,6 +173,12 @@ def roofline(db, key, kernel, ms, seg, smp, pix, full_smp):
         r["hbm_counter"] = {"achieved": round(g, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                             "frac": round(g / PEAK_HBM_GBS, 4),
                             "bytes_per_launch": hbm, "source": "FETCH_SIZE*2 + WRITE_SIZE"}
+        lo = pmc.get("hbm_bytes_per_launch_uncorrected")
+        if lo:
+            # FETCH_SIZE undercounts 128-B requests by 2 but counts 64-B ones exactly
+            # (profiles/r3_fetch_calib: per-lane 128-B node gathers x2, 64-B leaf records
+            # x1), so the kernel's bytes lie between the uncorrected and corrected sums
+            r["hbm_counter"]["bytes_per_launch_range"] = [round(lo * share), round(hbm)]
     r["hbm_model"] = {"achieved": round(model_gbs, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                       "frac": round(model_gbs / PEAK_HBM_GBS, 4),
                       "bytes_per_launch": model_bytes,

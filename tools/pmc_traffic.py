@@ -7,8 +7,12 @@ per-config counters <tag>_pmc_<config>.json, all written to gpurun_out/profiles_
 
   FETCH_SIZE / WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE reads exactly half
   the bytes of a wide coalesced streaming read (the guide's correction: double
-  it); for other access widths it is uncalibrated, so both the raw and the
-  corrected figure are recorded.  Counters are collected in runs of their own
+  it).  Calibrated for the traversal's gathers (tools/fetch_calib.hip,
+  profiles/r3_fetch_calib/): per-lane 128-B line gathers also read half (x2),
+  per-lane 64-B gathers read exactly (x1, and the HBM moves 64 B: a 64-B gather
+  over distinct lines takes half the time of the 128-B one).  A kernel mixing
+  both (BVH nodes 128 B, leaf records 64 B) lies between the raw and the
+  corrected figure; both are recorded.  Counters are collected in runs of their own
   (kernel-trace only), never combined with sys/runtime tracing.
 
 usage (on the GPU box, from the repo root):
