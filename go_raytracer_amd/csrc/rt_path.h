@@ -189,12 +189,35 @@ RT_D Ids chunk_ids(const Params& P, uint32_t chunk) {
 // VGPR lanes, one v_readlane per use).  [0] pixel00 - center | 1/s, [1] du | fd_s.m,
 // [2] dv | fd_s shifts, [3] center | s, [4] defocus u | defocus flag, [5] defocus v.
 __shared__ F4 g_cam[6];
-// Kernels that read the camera from g_cam: the book2 and mesh sets (C4 -3.6 %, C5 -2.3 %,
-// fewer SGPR and VGPR spills); the C2 and C3 kernels lose from it (their VGPR budget
-// takes the loaded constants: C2 +26 %), they keep them in SGPRs
+// Kernels that read the camera from g_cam (round 2, against SGPR-resident constants): the
+// book2 and mesh sets (C4 -3.6 %, C5 -2.3 %, fewer SGPR and VGPR spills); the C2 and C3
+// kernels lost from it (their VGPR budget takes the loaded constants: C2 +26 %)
 constexpr bool cam_lds(uint32_t ft) {
   return ft == (FT_SPHERE | FT_TRI | FT_METAL) ||
          ft == (FT_SPHERE | FT_METAL | FT_DIEL | FT_MEDIA | FT_IMAGE | FT_NOISE);
+}
+// Where a kernel reads the camera constants: 1 = g_cam (book2 set), 2 = scalar loads from
+// the kernel-argument segment where a ray starts (kparams: SGPRs live only there), 0 = the
+// SGPRs the compiler holds P in for the whole kernel (A/B builds: -DRT_CAM_SGPR).  Against
+// 0, mode 2 took C2's SGPR spills to VGPR lanes from 78 to 34 and C3's from 101 to 32: C2
+// -1.9 / -4.6 %, C3 -2.1 / -2.5 % (two boxes); against 1, C5 -2.0 / -2.2 % but C4 +1.1 %
+// (profiles/r3_cam_kernarg_ab.jsonl); images bit-identical.
+constexpr int cam_mode(uint32_t ft) {
+#ifdef RT_CAM_SGPR
+  return cam_lds(ft) ? 1 : 0;
+#else
+  return ft == (FT_SPHERE | FT_METAL | FT_DIEL | FT_MEDIA | FT_IMAGE | FT_NOISE) ? 1 : 2;
+#endif
+}
+typedef __attribute__((address_space(4))) const Params cst_params;
+// The launch parameters re-read through the scalar cache where they are used: the asm
+// barrier hides that the pointer is the kernel-argument segment's, so the compiler
+// cannot hoist the loads to the kernel entry and hold the values in SGPRs across the
+// whole loop (where they spill to VGPR lanes).
+RT_D const cst_params* kparams() {
+  const cst_params* p = (const cst_params*)__builtin_amdgcn_kernarg_segment_ptr();
+  __asm__ volatile("" : "+s"(p));
+  return p;
 }
 RT_D void stage_camera(const Params& P) {  // before a __syncthreads of every thread
   if (threadIdx.x == 0) {
@@ -209,18 +232,29 @@ RT_D void stage_camera(const Params& P) {  // before a __syncthreads of every th
 
 // getRay camera.go:256-270 + sampleSquareStratified :277-282 + defocusDiskSample :285-290;
 // r = rt_rng_draw(seed, gpix, sample, RT_STREAM_CAMERA), drawn by the caller.
-// CAM: the constants from g_cam (kernels that stage it, cam_lds) or from P.
-template <bool CAM>
+// CAM: where the constants come from (cam_mode): P (0), g_cam (1) or the kernarg segment (2).
+template <int CAM>
 RT_D void camera_ray_r(const Params& P, const Ids& id, uint32_t sample, const rt_u32x4& r, f3& o,
                        f3& d, float& time) {
   F4 c0, c1, c2, c3;
   FastDiv fd_s;
   uint32_t s;
-  if (CAM) {
+  bool defocus;
+  if constexpr (CAM == 1) {
     c0 = ld_lds(&g_cam[0]), c1 = ld_lds(&g_cam[1]), c2 = ld_lds(&g_cam[2]), c3 = ld_lds(&g_cam[3]);
     const uint32_t sh = fbits(c2.w);
     s = fbits(c3.w);
     fd_s = {fbits(c1.w), sh & 0xFFu, sh >> 8, s};
+    defocus = fbits(ld_lds(&g_cam[4]).w) != 0u;
+  } else if constexpr (CAM == 2) {
+    const cst_params* kp = kparams();
+    c0 = {kp->p00r[0], kp->p00r[1], kp->p00r[2], kp->recip_s};
+    c1 = {kp->du[0], kp->du[1], kp->du[2], 0.0f};
+    c2 = {kp->dv[0], kp->dv[1], kp->dv[2], 0.0f};
+    c3 = {kp->cc[0], kp->cc[1], kp->cc[2], 0.0f};
+    fd_s = {kp->fd_s.m, kp->fd_s.s1, kp->fd_s.s2, kp->fd_s.d};
+    s = (uint32_t)kp->s;
+    defocus = kp->defocus != 0;
   } else {
     c0 = {P.p00r[0], P.p00r[1], P.p00r[2], P.recip_s};
     c1 = {P.du[0], P.du[1], P.du[2], 0.0f};
@@ -228,6 +262,7 @@ RT_D void camera_ray_r(const Params& P, const Ids& id, uint32_t sample, const rt
     c3 = {P.cc[0], P.cc[1], P.cc[2], 0.0f};
     fd_s = P.fd_s;
     s = (uint32_t)P.s;
+    defocus = P.defocus != 0;
   }
   uint32_t si = fdiv(sample, fd_s), sj = sample - si * s;
   float px = (((float)sj + rt_unit_f(r.v[0])) * c0.w) - 0.5f;
@@ -237,9 +272,18 @@ RT_D void camera_ray_r(const Params& P, const Ids& id, uint32_t sample, const rt
   // the same vector without fp32 cancellation against large camera coordinates
   d = mk3(c0.x + c1.x * fx + c2.x * fy, c0.y + c1.y * fx + c2.y * fy, c0.z + c1.z * fx + c2.z * fy);
   o = mk3(c3.x, c3.y, c3.z);
-  if (CAM ? fbits(ld_lds(&g_cam[4]).w) != 0u : P.defocus != 0) {
-    const F4 c4 = CAM ? ld_lds(&g_cam[4]) : F4{P.dku[0], P.dku[1], P.dku[2], 0.0f};
-    const F4 c5 = CAM ? ld_lds(&g_cam[5]) : F4{P.dkv[0], P.dkv[1], P.dkv[2], 0.0f};
+  if (defocus) {
+    F4 c4, c5;
+    if constexpr (CAM == 1) {
+      c4 = ld_lds(&g_cam[4]), c5 = ld_lds(&g_cam[5]);
+    } else if constexpr (CAM == 2) {
+      const cst_params* kp = kparams();
+      c4 = {kp->dku[0], kp->dku[1], kp->dku[2], 0.0f};
+      c5 = {kp->dkv[0], kp->dkv[1], kp->dkv[2], 0.0f};
+    } else {
+      c4 = {P.dku[0], P.dku[1], P.dku[2], 0.0f};
+      c5 = {P.dkv[0], P.dkv[1], P.dkv[2], 0.0f};
+    }
     rt_u32x4 q = rt_rng_draw(P.seed, id.gpix, sample, RT_STREAM_CAMERA | 1u);
     f3 dk = uniform_disk(rt_unit_f(q.v[0]), rt_unit_f(q.v[1]));
     f3 off = mk3(c4.x, c4.y, c4.z) * dk.x + mk3(c5.x, c5.y, c5.z) * dk.y;
@@ -1372,7 +1416,7 @@ RT_D void load_path(const Params& P, uint32_t slot, Path& s) {
 
 // the next sample of the same chunk, its camera draw already made: the path
 // state (pixel ids cached in s) is reset for sample j
-template <bool SOA, bool CAM = false>
+template <bool SOA, int CAM = 0>
 RT_D void next_sample(const Params& P, uint32_t slot, Path& s, uint32_t j, const rt_u32x4& r) {
   Ids id;
   id.gpix = s.gpix;
@@ -1388,7 +1432,7 @@ RT_D void next_sample(const Params& P, uint32_t slot, Path& s, uint32_t j, const
 }
 
 // camera ray for sample j of `chunk` (path state reset)
-template <bool SOA, bool CAM = false>
+template <bool SOA, int CAM = 0>
 RT_D void start_sample(const Params& P, uint32_t slot, Path& s, uint32_t chunk, uint32_t j) {
   Ids id = chunk_ids(P, chunk);
   const rt_u32x4 r = rt_rng_draw(P.seed, id.gpix, id.sample0 + j, RT_STREAM_CAMERA);
@@ -1644,7 +1688,7 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
   if (s.j + 1 < count) {
     if (!have_rcam)  // a miss, or the depth limit: the camera draw is made here
       rcam = rt_rng_draw(P.seed, s.gpix, s.s0 + s.j + 1, RT_STREAM_CAMERA);
-    next_sample<SOA, cam_lds(FT)>(P, slot, s, s.j + 1, rcam);
+    next_sample<SOA, cam_mode(FT)>(P, slot, s, s.j + 1, rcam);
     PH_ADD(PH_TERM, t_term);
     return OUT_ALIVE;
   }

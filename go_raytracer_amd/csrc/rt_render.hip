@@ -261,7 +261,7 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
   __shared__ unsigned long long lacc[3 * 256];  // per-lane chunk sums (SampleAcc)
   for (int ch = 0; ch < 3; ++ch) lacc[ch * 256 + threadIdx.x] = 0ull;
   if constexpr (HAS(FT_NOISE)) stage_perlin(P.sc);  // before stage_nodes' barrier
-  if constexpr (cam_lds(FT)) stage_camera(P);
+  if constexpr (cam_mode(FT) == 1) stage_camera(P);
   const bool recs_lds = LDS && TREE != 8 && stage_nodes(P, lnodes, TREE == 4 ? 8 : 4);
   if (!LDS) __syncthreads();  // staged tables visible to every wave (stage_nodes ends with one)
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;  // weight-stack column
@@ -293,7 +293,7 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
     PH_T(t_grab);
     const uint32_t c = grab_chunk(P, b, !has);
     if (c != 0xFFFFFFFFu) {
-      start_sample<false, cam_lds(FT)>(P, slot, s, c, 0);
+      start_sample<false, cam_mode(FT)>(P, slot, s, c, 0);
       trav_init(P.sc, s.d, tr);
       has = true;
     }
