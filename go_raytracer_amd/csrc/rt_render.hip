@@ -216,8 +216,16 @@ constexpr int fused_waves(uint32_t ft, int tree = 4) {
 #ifndef MESH_SHORT
 #define MESH_SHORT 16  // C5's 1M-triangle tree: -1.3 % against 12 (r2_mesh_short_ab.jsonl)
 #endif
+#ifndef TRI_SHORT
+#define TRI_SHORT MESH_SHORT  // the {sphere, triangle, metal} set (C5)
+#endif
+#ifndef TRI_WLDS
+#define TRI_WLDS MESH_WLDS
+#endif
 #ifndef TEX_SHORT
-#define TEX_SHORT kShortStack
+// book2's set: 13 entries fill its 4-wave LDS budget (C4 -1.0 % against 12 at full size;
+// 16 x 3 / 18 x 2 / 21 x 1 stack x weight entries: +0.6 to +1.7 %, r3_tex_stack_ab.jsonl)
+#define TEX_SHORT 13
 #endif
 #ifndef TEX_WLDS
 #define TEX_WLDS 4  // book2's set: room for the staged perlin tables at 4 waves/SIMD
@@ -229,8 +237,8 @@ constexpr int fused_waves(uint32_t ft, int tree = 4) {
 #define BRUTE_WLDS kLdsWMax
 #endif
 constexpr int fused_wlds(uint32_t ft, int tree = 4) {
-  return (ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ||
-          ft == (FT_SPHERE | FT_TRI | FT_METAL)) ? MESH_WLDS
+  return ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? MESH_WLDS
+         : ft == (FT_SPHERE | FT_TRI | FT_METAL)                    ? TRI_WLDS
          : (ft == 0u && tree != 0)                                  ? 4
          : (ft == 0u && tree == 0)                                  ? BRUTE_WLDS
          : ft == FT_ALL                                             ? ALL_WLDS
@@ -242,8 +250,8 @@ constexpr int fused_wlds(uint32_t ft, int tree = 4) {
 constexpr int fused_short(uint32_t ft, int tree = 4) {
   return tree == 0                                                    ? 0
          : ft == 0u                                                   ? kShortStackMin
-         : (ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ||
-            ft == (FT_SPHERE | FT_TRI | FT_METAL)) ? MESH_SHORT
+         : ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? MESH_SHORT
+         : ft == (FT_SPHERE | FT_TRI | FT_METAL)                      ? TRI_SHORT
          : ft == (FT_SPHERE | FT_METAL | FT_DIEL | FT_MEDIA | FT_IMAGE | FT_NOISE) ? TEX_SHORT
                                                                       : kShortStack;
 }

@@ -3,7 +3,7 @@
 #   tests    pytest -m gpu (PARITY_LOG -> gpurun_out/parity_TAG.jsonl)
 #   ab       tools/ab_configs.sh: build_prev vs in-tree library, alternating, C2-C5
 #   configs  tools/probe_configs.sh: C2-C5 at full size, one render each
-#   bench    bench.py (default flags) -> gpurun_out/bench_TAG.json
+#   bench    bench.py (default flags; the pmc step's traffic.json when it ran first) -> gpurun_out/bench_TAG.json
 #   prof     rocprofv3 --kernel-trace --stats of bench.py -> gpurun_out/prof_TAG/
 #   share    tools/share_probe.py for cornell, book2, model
 #   pmc      tools/pmc_traffic.py TAG C2 C3 C4 C5 -> profiles/traffic.json + profiles/TAG_pmc_*.json
@@ -22,7 +22,8 @@ for step in "$@"; do
              --timeout 300 --timeout-method thread > "$O/tests_$TAG.log" 2>&1 ;;
     ab) timeout -k 10 900 bash tools/ab_configs.sh "$O/ab_$TAG.jsonl" ;;
     configs) timeout -k 10 600 bash tools/probe_configs.sh "$O/configs_$TAG.jsonl" ;;
-    bench) timeout -k 10 600 python3 bench.py > "$O/bench_$TAG.json" 2> "$O/bench_$TAG.err" ;;
+    bench) T=$O/profiles_$TAG/traffic.json; BA=(); [ -f "$T" ] && BA=(--traffic "$T")
+           timeout -k 10 600 python3 bench.py "${BA[@]}" > "$O/bench_$TAG.json" 2> "$O/bench_$TAG.err" ;;
     prof) (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d "$O/prof_$TAG" \
              -o run -- python3 "$R/bench.py" --no-cpu-baseline --steps 5 > "$O/prof_$TAG.log" 2>&1) ;;
     share) for s in "cornell 800 1024" "book2 800 4096" "model 1920 1024"; do
