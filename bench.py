@@ -74,7 +74,47 @@ def parse():
                          "one RCCL ncclGather (RT_FLAG_GATHER_RCCL; distinct devices)")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"),
                     help="PMC counters per launch (tools/pmc_traffic.py)")
+    ap.add_argument("--no-multi-check", action="store_true",
+                    help="torchrun jobs: skip rank 0's rt_render_multi check over distinct devices")
+    ap.add_argument("--multi-device-check", type=int, default=0, metavar="N",
+                    help=argparse.SUPPRESS)  # child-process mode of that check
     return ap.parse_args()
+
+
+def multi_device_check(ndev):
+    """rt_render_multi over DISTINCT devices 0..ndev-1 -- the Go-host path (peer access, peer
+    copies into devices[0], one scene upload per device, the RCCL ncclGather option) --
+    compared bit for bit with a one-device rt_render of the same image.  A torchrun job on a
+    multi-GPU node runs it in a child process of rank 0 after the timed regions, so a
+    failure cannot cost the bench line; a one-GPU box has no distinct devices to use."""
+    import numpy as np
+    import go_raytracer_amd as rt
+    res = {"devices": list(range(ndev))}
+    t, cam, w, l = rt.demo_scene("cornell")
+    cam.Width, cam.SamplesPerPixel = 96, 16
+    with rt.Scene(t, w, l) as sc:
+        ref, _ = sc.render(cam, seed=5, device=0)
+        for name, devs, rccl in (("peer", list(range(ndev)), False),
+                                 ("peer_reversed", list(range(ndev))[::-1], False),
+                                 ("rccl", list(range(ndev)), True)):
+            t0 = time.perf_counter()
+            img, _ = sc.render_multi(cam, devs, seed=5, rccl=rccl)
+            res[name] = {"bitwise": bool(np.array_equal(ref.view(np.uint32), img.view(np.uint32))),
+                         "s": round(time.perf_counter() - t0, 3)}
+    return res
+
+
+def run_multi_device_check(ndev):
+    import subprocess
+    try:
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--multi-device-check",
+                            str(ndev)], capture_output=True, text=True, timeout=180)
+        out = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        if r.returncode == 0 and out:
+            return json.loads(out[-1])
+        return {"devices": list(range(ndev)), "error": f"exit {r.returncode}: {r.stderr[-300:]}"}
+    except Exception as e:  # timeout or spawn failure
+        return {"devices": list(range(ndev)), "error": str(e)[:300]}
 
 
 def cpu_model():
@@ -194,6 +234,9 @@ def roofline(db, key, kernel, ms, seg, smp, pix, full_smp):
 
 def main():
     args = parse()
+    if args.multi_device_check:
+        print(json.dumps(multi_device_check(args.multi_device_check)), flush=True)
+        return
     import torch
     import torch.distributed as dist
 
@@ -420,6 +463,11 @@ def main():
             line["speedup_vs_cpu"] = round(line["value"] / cpu["value"], 1)
             line["speedup_vs_host_extrapolated"] = round(
                 line["value"] / cpu["host"]["extrapolated_all_cores_Msamples_s"], 1)
+        if world_size > 1 and not args.no_multi_check:
+            ndev = torch.cuda.device_count()
+            line["checks"] = {"render_multi_distinct_devices":
+                              run_multi_device_check(min(ndev, 8)) if ndev >= 2 else
+                              {"skipped": f"{ndev} visible device(s)"}}
         print(json.dumps(line), flush=True)
     if world_size > 1:
         dist.destroy_process_group()

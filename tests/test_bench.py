@@ -52,3 +52,16 @@ def test_devices_mode_rccl_gather_line(gpu):
 def test_gather_option_rejects_unknown():
     p = _bench("--gather", "nccl-allgather")
     assert p.returncode != 0 and "invalid choice" in p.stderr
+
+
+@pytest.mark.gpu
+def test_multi_device_check_child_mode(gpu):
+    """bench.py's distinct-device check (run by rank 0 of a torchrun job on a multi-GPU
+    node) in its child-process mode; on one GPU the device list is [0]."""
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--multi-device-check",
+                        "1"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res["devices"] == [0]
+    for k in ("peer", "peer_reversed", "rccl"):
+        assert res[k]["bitwise"], res
