@@ -1706,6 +1706,10 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
 struct WaveBatch {
   uint32_t next, end;  // wave-uniform
 };
+// SGB: the leader's atomic result read into an SGPR (v_readlane, no LDS permute) and the
+// batch bounds kept wave-uniform in SGPRs instead of VGPRs: C2 -0.6 % (its 4 spilled VGPRs
+// gone), C5 -1.6 %, C3 -0.1 %, but C4 +0.8 % (r3_batch_sgpr_ab.jsonl; bit-identical)
+template <bool SGB>
 RT_D uint32_t grab_chunk(const Params& P, WaveBatch& b, bool need) {
   const unsigned long long m = __ballot(need);
   if (!m) return 0xFFFFFFFFu;
@@ -1715,17 +1719,25 @@ RT_D uint32_t grab_chunk(const Params& P, WaveBatch& b, bool need) {
   uint32_t mine;
   if (n <= avail) {
     mine = b.next + r;
-    b.next += n;
+    if (SGB) b.next = __builtin_amdgcn_readfirstlane(b.next + n);
+    else b.next += n;
   } else {
     // (smaller batches over the last part of the range measured 4-15 % slower,
     // even over its last 0.5 %: profiles/r1_wave_timeline.jsonl, r1_tail_sweep.jsonl)
     const uint32_t grab = max(P.grab_min, n - avail);
     uint32_t g = 0;
     if (lane_id() == (uint32_t)(__ffsll((long long)m) - 1)) g = atomicAdd(&P.ctr->chunk_head, grab);
-    g = __shfl(g, __ffsll((long long)m) - 1);
-    mine = r < avail ? b.next + r : g + (r - avail);
-    b.next = g + (n - avail);
-    b.end = g + grab;
+    if (SGB) {
+      g = __builtin_amdgcn_readlane(g, __ffsll((long long)m) - 1);
+      mine = r < avail ? b.next + r : g + (r - avail);
+      b.next = __builtin_amdgcn_readfirstlane(g + (n - avail));
+      b.end = __builtin_amdgcn_readfirstlane(g + grab);
+    } else {
+      g = __shfl(g, __ffsll((long long)m) - 1);
+      mine = r < avail ? b.next + r : g + (r - avail);
+      b.next = g + (n - avail);
+      b.end = g + grab;
+    }
   }
   if (!need) return 0xFFFFFFFFu;
   return mine < P.n_chunks ? mine : 0xFFFFFFFFu;

@@ -299,7 +299,8 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
   PH_T(t_loop);
   for (;;) {
     PH_T(t_grab);
-    const uint32_t c = grab_chunk(P, b, !has);
+    const uint32_t c =
+        grab_chunk<FT != (FT_SPHERE | FT_METAL | FT_DIEL | FT_MEDIA | FT_IMAGE | FT_NOISE)>(P, b, !has);
     if (c != 0xFFFFFFFFu) {
       start_sample<false, cam_mode(FT)>(P, slot, s, c, 0);
       trav_init(P.sc, s.d, tr);
