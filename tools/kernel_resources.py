@@ -12,14 +12,21 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "..", "go_raytracer_amd", "csrc")
 
 
+# rt_fused_sets.hip's own flags (Makefile FUSED_SETS_FLAGS)
+SETS_FLAGS = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
+
+
 def main(argv):
-    src = argv[0] if argv and argv[0].endswith(".hip") else "rt_render.hip"
+    srcs = [a for a in argv if a.endswith(".hip")] or ["rt_render.hip", "rt_fused_sets.hip"]
     extra = [a for a in argv if not a.endswith(".hip")]
-    cmd = ["/opt/rocm/bin/hipcc", "-DBRUTE_WAVES=6", "-O3", "-std=c++17", "--offload-arch=gfx950",
-           "-I../../include", "-I.", "-Wno-unused-result", "-fno-hip-fp32-correctly-rounded-divide-sqrt",
-           "--cuda-device-only", "-c", src, "-o", "/tmp/_kr.o",
-           "-Rpass-analysis=kernel-resource-usage"] + extra
-    out = subprocess.run(cmd, cwd=CSRC, capture_output=True, text=True).stderr
+    out = ""
+    for src in srcs:
+        cmd = ["/opt/rocm/bin/hipcc", "-DBRUTE_WAVES=6", "-O3", "-std=c++17", "--offload-arch=gfx950",
+               "-I../../include", "-I.", "-Wno-unused-result",
+               "-fno-hip-fp32-correctly-rounded-divide-sqrt", "--cuda-device-only", "-c", src,
+               "-o", "/tmp/_kr.o", "-Rpass-analysis=kernel-resource-usage"] + extra + \
+              (SETS_FLAGS if src == "rt_fused_sets.hip" else [])
+        out += subprocess.run(cmd, cwd=CSRC, capture_output=True, text=True).stderr
     rows, cur = [], None
     for line in out.splitlines():
         m = re.search(r"remark: (.*?): (.*?) \[-Rpass", line)
