@@ -58,6 +58,11 @@ typedef struct {
 
 RT_RNG_FN rt_u32x4 rt_philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                     uint32_t k0, uint32_t k1) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(RT_RNG_ROLLED)
+  /* ten rounds straight-line (the compiler kept a loop of three): C3 -0.5 %, C4 -0.5 %,
+     C5 -0.4 %, C2 +-0, same words (profiles/r3_rng_unroll_ab.jsonl) */
+#pragma unroll
+#endif
   for (int r = 0; r < 10; ++r) {
     if (r) {
       k0 += RT_PHILOX_W0;
