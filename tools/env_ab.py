@@ -16,7 +16,7 @@ var, out_path, specs = sys.argv[1], sys.argv[2], sys.argv[3:]
 vals = (0, 1)
 if "=" in var:
     var, v = var.split("=")
-    vals = tuple(int(x) for x in v.split(","))
+    vals = tuple(v.split(","))
 
 
 def render(scene, width, spp, val, seed=3):
