@@ -54,5 +54,6 @@ def test_noise_tables_kernel_choice(rt, oracle, gpu, tables):
     ref, _ = oracle.render(t, world, lights, cam, seed=5, threads=8)
     assert (st["kernel_features"] == 255) == (tables > 1), st["kernel_features"]
     m = compare(img, ref)
+    # measured 0.9971 / 1.0 (profiles/r3_parity_v5.jsonl)
     assert m["frac_close"] >= 0.995, m
-    assert m["q_equal"] >= 0.99, m
+    assert m["q_equal"] >= 0.995, m
