@@ -85,7 +85,7 @@ class RtStats(C.Structure):
         ("ms_fused", C.c_double),
         ("kernel_features", C.c_int32), ("scene_features", C.c_int32),
         ("tree_width", C.c_int32), ("lds_scene", C.c_int32),
-        ("chunk_samples", C.c_int32), ("_pad2", C.c_int32),
+        ("chunk_samples", C.c_int32), ("record_boxes", C.c_int32),
         ("overflow_samples", C.c_uint64),
     ]
 

@@ -152,6 +152,10 @@ struct DevScene {
                         // the sides of boxes rotated about a), between the general and the
                         // axis-aligned pairs (rt_path.h brute_vert; only y is grouped: RotateY
                         // is the reference's only rotation, transformation.go:48)
+  int32_t brute_box;    // record loop: pairs of box descriptors after the axis-aligned pairs
+                        // (boxes rotated about y, tested as slabs: rt_path.h brute_box),
+                        // then the boxes' face records (not looped over)
+  int32_t brute_ng;     // record loop: general pairs (the first ones)
   int32_t n_perlins;    // perlin 0's tables are staged in LDS by the noise kernels
 };
 

@@ -806,6 +806,88 @@ RT_D void brute_vert(const DevScene& sc, const F4* lrec, int p0, int p1, const v
     bk = c1 ? k1 : bk;
   }
 }
+// Boxes rotated about y (host-detected: six records forming a box, rt_render.hip), two per
+// descriptor pair: C.x | C.z | ax/|ax|^2 | az/|az|^2 (x, z) | y range | face slots.  In the
+// box's frame (x' = (p - C).ax/|ax|^2, z' likewise, y unchanged) the faces are the planes
+// x' = 0 / 1, y = ylo / yhi, z' = 0 / 1, and each face's quad test is t = (k - o'_a) / d'_a:
+// the reference's own arithmetic in rotateY.Hit's object frame (transformation.go:94-107,
+// objects.go:102-118).  The closest face with t in [tmin, best] is the entering one when
+// t_near >= tmin, else the leaving one: one slab test instead of six record tests.  The
+// winner is recorded as a box code (pair, half, leaving) and resolved to its face record
+// after the loop (box_face).
+constexpr uint32_t kBoxCode = 0x40000000u;
+template <bool SMEM>
+RT_D void brute_box(const DevScene& sc, const F4* lrec, int p0, int p1, const v2f* O,
+                    const v2f* Dv, float iy1, float tmin, float& best, uint32_t& bk) {
+  const v2f iy = {iy1, iy1};
+  for (int p = p0; p < p1; ++p) {
+    v4f r[4];
+    if (SMEM) {
+      typedef __attribute__((address_space(4))) const v4f cst_v4;
+      const cst_v4* q = (const cst_v4*)sc.leafprims + 8 * __builtin_amdgcn_readfirstlane(p);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) r[e] = q[e];
+    } else {
+      const lds_v4* q = (const lds_v4*)lrec + 8 * p;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) r[e] = q[e];
+    }
+    const v2f ex = O[0] - r[0].xy, ez = O[2] - r[0].zw;
+    const v2f lx = pfma(ez, r[1].zw, ex * r[1].xy), lz = pfma(ez, r[2].zw, ex * r[2].xy);
+    const v2f vx = pfma(Dv[2], r[1].zw, Dv[0] * r[1].xy), vz = pfma(Dv[2], r[2].zw, Dv[0] * r[2].xy);
+    const v2f ix = {rcp(vx.x), rcp(vx.y)}, iz = {rcp(vz.x), rcp(vz.y)};
+    const v2f tx0 = -lx * ix, tx1 = pfma(-lx, ix, ix);
+    const v2f tz0 = -lz * iz, tz1 = pfma(-lz, iz, iz);
+    const v2f ty0 = (r[3].xy - O[1]) * iy, ty1 = (r[3].zw - O[1]) * iy;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float ax0 = h ? tx0.y : tx0.x, ax1 = h ? tx1.y : tx1.x;
+      const float ay0 = h ? ty0.y : ty0.x, ay1 = h ? ty1.y : ty1.x;
+      const float az0 = h ? tz0.y : tz0.x, az1 = h ? tz1.y : tz1.x;
+      const float tn = fmaxf(fmaxf(fminf(ax0, ax1), fminf(ay0, ay1)), fminf(az0, az1));
+      const float tf = fminf(fminf(fmaxf(ax0, ax1), fmaxf(ay0, ay1)), fmaxf(az0, az1));
+      const bool enter = tn >= tmin;
+      const float t = enter ? tn : tf;
+      const bool c = tn <= tf && t >= tmin && t <= best;
+      best = c ? t : best;
+      bk = c ? (kBoxCode | ((uint32_t)p << 2) | ((uint32_t)h << 1) | (enter ? 0u : 1u)) : bk;
+    }
+  }
+}
+// the face record slot of a box code: the plane (of the entering or leaving three) whose
+// t is the loop's winning t, recomputed with the loop's operations
+template <bool SMEM>
+RT_D uint32_t box_face(const DevScene& sc, const F4* lrec, uint32_t code, f3 o, f3 d, float iy,
+                       float best) {
+  const uint32_t base = 32u * ((code & ~kBoxCode) >> 2) + ((code >> 1) & 1u);
+  float f[14];
+  if (SMEM) {
+    const float* g = (const float*)sc.leafprims + base;
+#pragma unroll
+    for (int e = 0; e < 14; ++e) f[e] = *(const __attribute__((address_space(1))) float*)(g + 2 * e);
+  } else {
+    const lds_f32* l = (const lds_f32*)lrec + base;
+#pragma unroll
+    for (int e = 0; e < 14; ++e) f[e] = l[2 * e];
+  }
+  const float ex = o.x - f[0], ez = o.z - f[1];
+  const float lx = fmaf(ez, f[3], ex * f[2]), lz = fmaf(ez, f[5], ex * f[4]);
+  const float ix = rcp(fmaf(d.z, f[3], d.x * f[2])), iz = rcp(fmaf(d.z, f[5], d.x * f[4]));
+  const float t[6] = {-lx * ix, fmaf(-lx, ix, ix), (f[6] - o.y) * iy, (f[7] - o.y) * iy,
+                      -lz * iz, fmaf(-lz, iz, iz)};
+  const bool leave = (code & 1u) != 0u;
+  int face = 0;
+  float err = kInf;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    // entering plane of slab a: the smaller t; leaving: the larger
+    const int side = (t[2 * a + 1] < t[2 * a]) != leave ? 1 : 0;
+    const float e = fabsf(t[2 * a + side] - best);
+    face = e < err ? 2 * a + side : face;
+    err = fminf(e, err);
+  }
+  return __float_as_uint(f[8 + face]);
+}
 template <uint32_t FT, bool SMEM>
 RT_D void trav_brute(const DevScene& sc, const F4* lrec, f3 o, f3 d, float time, float tmin,
                      Trav& tr) {
@@ -813,7 +895,7 @@ RT_D void trav_brute(const DevScene& sc, const F4* lrec, f3 o, f3 d, float time,
   const int nax = sc.brute_ax[0], nay = sc.brute_ax[1], naz = sc.brute_ax[2];
   const int nvy = sc.brute_vt[1];  // y-parallel pairs only (RotateY is the only rotation)
   // general pairs first, then the y-parallel and the axis-aligned groups
-  const int ng = (sc.n_refs >> 1) - nax - nay - naz - nvy;
+  const int ng = sc.brute_ng;
   const v2f ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
   const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z};
   float best = tr.best.t;
@@ -846,7 +928,11 @@ RT_D void trav_brute(const DevScene& sc, const F4* lrec, f3 o, f3 d, float time,
   brute_axis<0, SMEM>(sc, lrec, q, q + nax, O, Dv, tmin, best, bk);
   brute_axis<1, SMEM>(sc, lrec, q + nax, q + nax + nay, O, Dv, tmin, best, bk);
   brute_axis<2, SMEM>(sc, lrec, q + nax + nay, q + nax + nay + naz, O, Dv, tmin, best, bk);
+  const int qb = q + nax + nay + naz;
+  const float iy = rcp(d.y);
+  brute_box<SMEM>(sc, lrec, qb, qb + sc.brute_box, O, Dv, iy, tmin, best, bk);
   if (bk != 0xFFFFFFFFu) {
+    if (bk & kBoxCode) bk = box_face<SMEM>(sc, lrec, bk, o, d, iy, best);
     // the winner's fields (pair bk/2, half bk&1): Q at floats 8/10/12, A at
     // 14/16/18, B at 20/22/24, ref at 28 (+ half)
     const uint32_t base = 32u * (bk >> 1) + (bk & 1u);

@@ -181,6 +181,7 @@ struct DeviceScene {
   const F4* nodes2 = nullptr;   // BVH2 of the same leaves (tiny scenes)
   const F4* brute_pairs = nullptr;  // quad records in pairs, largest first (record loop)
   size_t brute_slots = 0;           // records in brute_pairs, pads included (even)
+  int32_t brute_boxes = 0;          // boxes among them tested as slabs (rt_path.h brute_box)
   uint32_t root2 = PRIM_NONE;
   int32_t n_nodes2 = 0;
   ~DeviceScene() {
@@ -499,8 +500,102 @@ static int upload_scene(const Scene* s, DeviceScene* ds) {
       // y only (brute_vert<1>): RotateY is the reference's only rotation
       return n[1] == 0.0f && A[1] == 0.0f && B[0] == 0.0f && B[2] == 0.0f && B[1] != 0.0f ? 1 : -1;
     };
+    // Boxes rotated about y (NewBox objects.go:208-240 under RotateY / Translate,
+    // transformation.go:13-110; Cornell's two boxes): six quad records whose corners are
+    // the eight corners of one box with a horizontal top and bottom.  The loop tests each
+    // such box once, as three slabs in the box's own frame -- the reference's rotateY.Hit
+    // frame, where each face's quad test is t = (k - o'_a) / d'_a -- instead of its six
+    // records (rt_path.h brute_box).  The face records stay in the array (after the box
+    // descriptors) for the winner's u, v and ref.  RT_BRUTE_BOX=0 keeps them in the groups.
+    struct BoxRec { size_t face[6]; double C[3], ax[3], az[3], H; };
+    std::vector<BoxRec> boxes;
+    std::vector<char> in_box(h.refs.size(), 0);
+    if (env_int("RT_BRUTE_BOX", 1) != 0) {
+      auto qd = [&](size_t i, int k, double* out) {  // k: 0 Q, 1 u, 2 v
+        const F4& f = h.quad[5 * (size_t)(h.refs[i] & 0x3FFFFFFFu) + k];
+        out[0] = f.x, out[1] = f.y, out[2] = f.z;
+      };
+      auto corners = [&](size_t i, double P[4][3]) {
+        double Q[3], u[3], v[3];
+        qd(i, 0, Q), qd(i, 1, u), qd(i, 2, v);
+        for (int c = 0; c < 3; ++c) {
+          P[0][c] = Q[c], P[1][c] = Q[c] + u[c], P[2][c] = Q[c] + v[c];
+          P[3][c] = Q[c] + u[c] + v[c];
+        }
+      };
+      std::vector<size_t> quads;
+      for (size_t i : ord)
+        if ((h.refs[i] >> 30) == PRIM_QUAD) quads.push_back(i);
+      // four corners of quad i == the four points F (as sets, within tol)
+      auto same_face = [&](size_t i, const double F[4][3], double tol) {
+        double P[4][3];
+        corners(i, P);
+        bool used[4] = {false, false, false, false};
+        for (int a = 0; a < 4; ++a) {
+          int m = -1;
+          for (int b = 0; b < 4 && m < 0; ++b)
+            if (!used[b] && fabs(P[a][0] - F[b][0]) <= tol && fabs(P[a][1] - F[b][1]) <= tol &&
+                fabs(P[a][2] - F[b][2]) <= tol)
+              m = b;
+          if (m < 0) return false;
+          used[m] = true;
+        }
+        return true;
+      };
+      for (size_t i : quads) {
+        if (in_box[i]) continue;
+        double C[3], ax[3], az[3];
+        qd(i, 0, C), qd(i, 1, ax), qd(i, 2, az);
+        const double la = sqrt(ax[0] * ax[0] + ax[2] * ax[2]), lb = sqrt(az[0] * az[0] + az[2] * az[2]);
+        // a horizontal rectangle: the bottom (or top) face of a candidate box
+        if (ax[1] != 0.0 || az[1] != 0.0 || la == 0.0 || lb == 0.0 ||
+            fabs(ax[0] * az[0] + ax[2] * az[2]) > 1e-6 * la * lb)
+          continue;
+        const double tol = 1e-5 * (1.0 + fabs(C[0]) + fabs(C[1]) + fabs(C[2]) + la + lb);
+        auto corner = [&](int k, double H, double* out) {  // bit 0: +ax, 1: +az, 2: +H
+          for (int c = 0; c < 3; ++c)
+            out[c] = C[c] + ((k & 1) ? ax[c] : 0.0) + ((k & 2) ? az[c] : 0.0) + (c == 1 && (k & 4) ? H : 0.0);
+        };
+        // faces by (axis, side): x' = bit 0, y = bit 2, z' = bit 1
+        const int fbit[3] = {1, 4, 2};
+        for (size_t j : quads) {
+          if (j == i || in_box[j]) continue;
+          double Qj[3];
+          qd(j, 0, Qj);
+          const double H = Qj[1] - C[1];
+          if (fabs(H) <= tol) continue;
+          BoxRec b{};
+          bool ok = true;
+          for (int f = 0; f < 6 && ok; ++f) {
+            double F[4][3];
+            int n = 0;
+            for (int k = 0; k < 8; ++k)
+              if (((k & fbit[f >> 1]) != 0) == (f & 1)) corner(k, H, F[n++]);
+            size_t hit = (size_t)-1;
+            if (f == 2) hit = i;
+            else if (f == 3) hit = same_face(j, F, tol) ? j : (size_t)-1;
+            else
+              for (size_t m : quads)
+                if (m != i && m != j && !in_box[m] && same_face(m, F, tol)) {
+                  bool dup = false;
+                  for (int g = 0; g < f; ++g) dup |= b.face[g] == m;
+                  if (!dup) { hit = m; break; }
+                }
+            if (hit == (size_t)-1) ok = false;
+            else b.face[f] = hit;
+          }
+          if (!ok) continue;
+          for (int c = 0; c < 3; ++c) b.C[c] = C[c], b.ax[c] = ax[c], b.az[c] = az[c];
+          b.H = H;
+          for (int f = 0; f < 6; ++f) in_box[b.face[f]] = 1;
+          boxes.push_back(b);
+          break;
+        }
+      }
+    }
     std::vector<size_t> grp[7];  // 0-2: axis-aligned groups, 3: general, 4-6: axis-parallel
     for (size_t i : ord) {
+      if (in_box[i]) continue;
       const int a = axis_of(i);
       const int v = a < 0 ? vert_of(i) : -1;
       grp[a >= 0 ? a : v >= 0 ? 4 + v : 3].push_back(i);
@@ -515,6 +610,7 @@ static int upload_scene(const Scene* s, DeviceScene* ds) {
     std::vector<long> slots;  // record per slot in loop order, -1 = pad
     for (size_t i : grp[3]) slots.push_back((long)i);
     if (slots.size() & 1) slots.push_back(-1);
+    d.brute_ng = (int32_t)(slots.size() / 2);
     for (int a = 0; a < 3; ++a) {
       for (size_t i : grp[4 + a]) slots.push_back((long)i);
       d.brute_vt[a] = (int32_t)(grp[4 + a].size() / 2);
@@ -524,9 +620,39 @@ static int upload_scene(const Scene* s, DeviceScene* ds) {
       for (size_t i : grp[a]) slots.push_back((long)i);
       d.brute_ax[a] = (int32_t)(grp[a].size() / 2);
     }
-    if (slots.empty()) slots.assign(2, -1);
+    const size_t n_loop = slots.size();  // records the loop tests one by one
+    // box descriptors, two per pair slot (an odd box count repeats the last box: the
+    // same t and faces, so the winner is unchanged), then the six face records per box
+    const size_t nbp = (boxes.size() + 1) / 2;
+    d.brute_box = (int32_t)nbp;
+    ds->brute_boxes = (int32_t)boxes.size();
+    slots.insert(slots.end(), 2 * nbp, -2);
+    const size_t face0 = slots.size();
+    for (const BoxRec& b : boxes)
+      for (int f = 0; f < 6; ++f) slots.push_back((long)b.face[f]);
+    if (slots.empty()) {
+      slots.assign(2, -1);
+      d.brute_ng = 1;
+    }
     // pair layout (rt_device.h): records 2p, 2p+1 interleaved field by field
     std::vector<F4> pairs(4 * slots.size(), F4{0, 0, 0, 0});  // pad: n = 0, never hit
+    for (size_t k = 0; k < 2 * nbp; ++k) {
+      // rt_path.h brute_box: C.x, C.z, ax/|ax|^2 (x, z), az/|az|^2 (x, z), y range, faces
+      const BoxRec& b = boxes[std::min(k, boxes.size() - 1)];
+      float* f = (float*)&pairs[4 * (n_loop + k - (k & 1))] + (k & 1);
+      const double a2 = b.ax[0] * b.ax[0] + b.ax[2] * b.ax[2], z2 = b.az[0] * b.az[0] + b.az[2] * b.az[2];
+      const double y0 = b.C[1], y1 = b.C[1] + b.H;
+      const float v[8] = {(float)b.C[0], (float)b.C[2], (float)(b.ax[0] / a2), (float)(b.ax[2] / a2),
+                          (float)(b.az[0] / z2), (float)(b.az[2] / z2), (float)std::min(y0, y1),
+                          (float)std::max(y0, y1)};
+      for (int e = 0; e < 8; ++e) f[2 * e] = v[e];
+      for (int fc = 0; fc < 6; ++fc) {
+        // face slot by (axis x' / y / z', low / high side); y's low side is the lower face
+        const int src = (fc >> 1) == 1 && b.H < 0 ? (fc ^ 1) : fc;
+        const uint32_t slot = (uint32_t)(face0 + 6 * std::min(k, boxes.size() - 1) + src);
+        memcpy(&f[2 * (8 + fc)], &slot, 4);
+      }
+    }
     for (size_t i = 0; i < slots.size(); ++i) {
       if (slots[i] < 0) continue;
       const F4* r = &recs[4 * (size_t)slots[i]];  // Q|ref, n|D, A, B
@@ -535,7 +661,7 @@ static int upload_scene(const Scene* s, DeviceScene* ds) {
       const uint32_t k = (uint32_t)i;
       memcpy(&kb, &k, 4);
       // axis records: D / n_a (= +-D exactly) in the D slot, so t = (D' - o_a) / d_a
-      const int a = i >= n_general ? axis_of((size_t)slots[i]) : -1;
+      const int a = i >= n_general && i < n_loop ? axis_of((size_t)slots[i]) : -1;
       const float na = a == 0 ? r[1].x : a == 1 ? r[1].y : r[1].z;
       const float Dp = a < 0 ? r[1].w : na * r[1].w;
       const float v[15] = {r[1].x, r[1].y, r[1].z, Dp,     r[0].x, r[0].y, r[0].z, r[2].x,
@@ -1125,6 +1251,7 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     stats->scene_features = (int32_t)feats;
     stats->tree_width = tree;
     stats->chunk_samples = (int32_t)K;
+    stats->record_boxes = tree == 0 ? ds->brute_boxes : 0;
     stats->lds_scene = mode == RT_MODE_FUSED ? (f_lds ? 1 : 0) : (lds_nodes ? 1 : 0);
     auto sum_ms = [&](const std::vector<std::pair<int, int>>& v, double* acc) -> int {
       for (auto& pr : v) {

@@ -365,7 +365,7 @@ typedef struct {
   int32_t tree_width;      /* BVH arity the kernels traversed (2 or 4) */
   int32_t lds_scene;       /* 1: nodes (and leaf records) ran from the LDS cache */
   int32_t chunk_samples;   /* samples per work chunk (opts.chunk or the adaptive choice) */
-  int32_t _pad2;
+  int32_t record_boxes;    /* boxes the record loop tested as one slab test each (0: none) */
   /* sample channels with |v| >= 2^31 / spp_sqrt^2 (outside the exact fixed-point pixel
    * sum; added in fp64 instead — the image is then order-dependent in those pixels) */
   uint64_t overflow_samples;

@@ -150,9 +150,11 @@ def test_axis_record_groups_match_general_test(rt, gpu, monkeypatch, var, name):
     """The record loop's axis-aligned groups (rt_path.h brute_axis) and its y-parallel
     group (brute_vert: the rotated boxes' sides) compute the general quad test's t,
     alpha and beta bit for bit: the Cornell boxes render the same image with either
-    grouping switched off (RT_BRUTE_AXIS=0 / RT_BRUTE_VERT=0)."""
+    grouping switched off (RT_BRUTE_AXIS=0 / RT_BRUTE_VERT=0).  The boxes' records stay
+    in the loop here (RT_BRUTE_BOX=0): the slab test is checked below."""
     t, cam, w, l = rt.demo_scene(name)
     cam.Width, cam.SamplesPerPixel = 96, 64
+    monkeypatch.setenv("RT_BRUTE_BOX", "0")
     imgs = []
     for flag in ("0", "1"):
         monkeypatch.setenv(var, flag)
@@ -161,6 +163,29 @@ def test_axis_record_groups_match_general_test(rt, gpu, monkeypatch, var, name):
         assert st["tree_width"] == 0
         imgs.append(img)
     assert np.array_equal(imgs[0], imgs[1], equal_nan=True)
+
+
+@pytest.mark.parametrize("name", ["cornell", "cornell_smoke"])
+def test_record_loop_boxes(rt, oracle, gpu, monkeypatch, name):
+    """Boxes rotated about y are tested as one slab test each in the record loop
+    (rt_path.h brute_box, the reference's rotateY frame): Cornell's two boxes are found,
+    the smoke scene's boxes are media boundaries (not records), and the image agrees
+    with the oracle as closely as the six-records path does (RT_BRUTE_BOX=0)."""
+    t, cam, w, l = rt.demo_scene(name)
+    cam.Width, cam.SamplesPerPixel = 96, 64
+    ref, _ = oracle.render(t, w, l, cam, seed=4, threads=8)
+    ms, boxes = [], []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("RT_BRUTE_BOX", flag)
+        with rt.Scene(t, w, l) as sc:
+            img, st = sc.render(cam, seed=4)
+        assert st["tree_width"] == 0
+        boxes.append(st["record_boxes"])
+        ms.append(compare(img, ref))
+    assert boxes == [0, 2 if name == "cornell" else 0], boxes
+    for m in ms:
+        assert m["frac_close"] >= 0.995 and m["q_equal"] >= 0.995, ms
+    assert ms[1]["q_equal"] >= ms[0]["q_equal"] - 0.002, ms
 
 
 def test_render_multi_same_device_is_bitwise(rt, gpu):
