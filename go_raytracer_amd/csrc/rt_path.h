@@ -1697,7 +1697,11 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
         float pdf = 0.5f * lights_pdf<FT>(sc, p, ndir) + 0.5f * bsdf_pdf;
 #endif
         PH_ADD(PH_LIGHT, t_light);
-        weight = (att * spdf) * rcp(pdf);
+        // pdf >= 1e-30: a direction below the surface (spdf = 0) whose light pdf test just
+        // misses the light's edge (pdf = 0) weighs 0, not 0 * inf = NaN (camera.go:321-328
+        // divides by the mixture pdf; one sample in ~1e9 of C2 met this in fp32).  Any
+        // pdf > 1e-30 is untouched.
+        weight = (att * spdf) * rcp(fmaxf(pdf, 1e-30f));
         clamp_vertex = true;
       }
       // vertex bookkeeping (H1: the clamp is folded backwards at termination)
@@ -1787,6 +1791,9 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
   } else {
     L = mk3(0, 0, 0);
   }
+#ifdef RT_NAN_DEBUG
+  if (isnan(L.x) || isnan(L.y) || isnan(L.z)) printf("NAN gpix %u sample %u\n", s.gpix, s.s0 + s.j);
+#endif
   sa.add(P, s.chunk, L);
   const uint32_t count = min(P.K, P.ss - s.s0);  // chunk_ids().count
   if (s.j + 1 < count) {
