@@ -156,6 +156,7 @@ struct DevScene {
                         // (boxes rotated about y, tested as slabs: rt_path.h brute_box),
                         // then the boxes' face records (not looped over)
   int32_t brute_ng;     // record loop: general pairs (the first ones)
+  float pdf_floor;      // 1e-30 when every light entry is a prim, else 0 (rt_path.h shade)
   int32_t n_perlins;    // perlin 0's tables are staged in LDS by the noise kernels
 };
 

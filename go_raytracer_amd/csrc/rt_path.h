@@ -1697,11 +1697,13 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
         float pdf = 0.5f * lights_pdf<FT>(sc, p, ndir) + 0.5f * bsdf_pdf;
 #endif
         PH_ADD(PH_LIGHT, t_light);
-        // pdf >= 1e-30: a direction below the surface (spdf = 0) whose light pdf test just
-        // misses the light's edge (pdf = 0) weighs 0, not 0 * inf = NaN (camera.go:321-328
-        // divides by the mixture pdf; one sample in ~1e9 of C2 met this in fp32).  Any
-        // pdf > 1e-30 is untouched.
-        weight = (att * spdf) * rcp(fmaxf(pdf, 1e-30f));
+        // pdf >= 1e-30 when every light entry is a prim (sc.pdf_floor): a direction below
+        // the surface (spdf = 0) whose light pdf test just misses the light's edge in fp32
+        // (pdf = 0) weighs 0, not 0 * inf = NaN (camera.go:321-328 divides by the mixture
+        // pdf; one sample in ~1e9 of C2 met this).  Any pdf > 1e-30 is untouched.  An empty
+        // lights list's pdf is 0 by the reference's rules (hittable.go:89-103): its 0/0 NaNs
+        // are the reference's own and stay (floor 0, test_world_without_lights_list).
+        weight = (att * spdf) * rcp(fmaxf(pdf, sc.pdf_floor));
         clamp_vertex = true;
       }
       // vertex bookkeeping (H1: the clamp is folded backwards at termination)

@@ -686,6 +686,11 @@ records_done:
   d.n_media = (int32_t)h.media.size();
   d.medium_draws = h.medium_draws;
   d.n_lights = (int32_t)h.lights.size();
+  // mixture-pdf floor (rt_path.h): only when every light entry is a real prim; an entry of
+  // an empty HittableList has pdf 0 by the reference's rules, and its 0/0 NaNs are kept
+  d.pdf_floor = h.lights.empty() ? 0.0f : 1e-30f;
+  for (const auto& e : h.lights)
+    if (e.ref == PRIM_NONE) d.pdf_floor = 0.0f;
   d.n_refs = (int32_t)h.refs.size();
   d.n_perlins = (int32_t)h.perlins.size();
   return RT_OK;
