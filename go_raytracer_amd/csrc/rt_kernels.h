@@ -76,7 +76,9 @@ RT_D Onb make_onb(f3 n) {
   o.w = unit(n);
   f3 a = fabsf(n.x) > 0.9f ? mk3(0, 1, 0) : mk3(1, 0, 0);
   o.v = unit(cross(n, a));
-  o.u = unit(cross(n, o.v));
+  // unit(cross(n, v)) = cross(n, v) / |n| = cross(w, v): w and v are unit and orthogonal, so
+  // the reference's third normalisation (onb.go:23) is the identity up to rounding
+  o.u = cross(o.w, o.v);
   return o;
 }
 RT_D f3 onb_transform(const Onb& o, f3 v) { return o.u * v.x + o.v * v.y + o.w * v.z; }  // :38-43
