@@ -531,6 +531,13 @@ int flatten_scene(const Tree& t, int world, int lights, HostScene& out) {
   if (b8 && atoi(b8) != 0 && out.refs.size() >= kBvh8MinRefs) {
     t0 = std::chrono::steady_clock::now();
     rc = build_bvh8(out);
+    if (rc != RT_OK) {
+      // an opt-in performance path never fails a valid scene: keep the BVH4
+      fprintf(stderr, "[rt] RT_BVH8: %s; keeping the BVH4\n", rt_last_error());
+      out.nodes8.clear();
+      out.refs8.clear();
+      rc = RT_OK;
+    }
     if (timing)
       fprintf(stderr, "[rt] build_bvh8 %.3f s (%zu nodes)\n",
               std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(),

@@ -158,6 +158,10 @@ struct DevScene {
   int32_t brute_ng;     // record loop: general pairs (the first ones)
   float pdf_floor;      // 1e-30 when every light entry is a prim, else 0 (rt_path.h shade)
   int32_t n_perlins;    // perlin 0's tables are staged in LDS by the noise kernels
+  int32_t merge_ok;     // every weight and radiance is >= 0 (solid colours, metal albedos
+                        // and, per render, the background): dominated clamp vertices may
+                        // be merged (rt_path.h shade_core); else each vertex is pushed
+  int32_t _pad_sc;
 };
 
 }  // namespace rt

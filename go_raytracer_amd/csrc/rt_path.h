@@ -1720,8 +1720,11 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
           // `pre`, which the book2 kernel keeps in scratch, cost more than it saved).
           // Same folded value up to fp32 rounding; paths through the water orb and
           // the fog (book2, up to 40 isotropic vertices) keep most of their stack in LDS.
-          const bool merge = s.nst > 0 && pv.x >= 0.0f && pv.y >= 0.0f && pv.z >= 0.0f &&
-                             pv.x <= 1.0f && pv.y <= 1.0f && pv.z <= 1.0f;
+          // Needs P_k+1 >= 0 in every channel: scenes with a negative colour, albedo or
+          // background (sc.merge_ok = 0) push every vertex, which the fold handles exactly
+          // for any sign.
+          const bool merge = sc.merge_ok && s.nst > 0 && pv.x >= 0.0f && pv.y >= 0.0f &&
+                             pv.z >= 0.0f && pv.x <= 1.0f && pv.y <= 1.0f && pv.z <= 1.0f;
 #else
           const bool merge = false;
 #endif

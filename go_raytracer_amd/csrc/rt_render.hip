@@ -693,6 +693,16 @@ records_done:
     if (e.ref == PRIM_NONE) d.pdf_floor = 0.0f;
   d.n_refs = (int32_t)h.refs.size();
   d.n_perlins = (int32_t)h.perlins.size();
+  // the weight merge needs non-negative suffix products: every texture value (solid
+  // colours; image and noise values are >= 0 by construction) and metal albedo >= 0
+  // (the background is checked per render)
+  d.merge_ok = 1;
+  for (const auto& t : h.texs)
+    if (t.kind == RT_TEX_SOLID && !(t.color.x >= 0.0f && t.color.y >= 0.0f && t.color.z >= 0.0f))
+      d.merge_ok = 0;
+  for (const auto& m : mats)
+    if (m.kind == RT_MAT_METAL && !(m.albedo.x >= 0.0f && m.albedo.y >= 0.0f && m.albedo.z >= 0.0f))
+      d.merge_ok = 0;
   return RT_OK;
 }
 
@@ -987,6 +997,7 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     p.dkv[i] = (float)cd.defocus_v[i];
     p.bg[i] = (float)cd.background[i];
   }
+  if (!(p.bg[0] >= 0.0f && p.bg[1] >= 0.0f && p.bg[2] >= 0.0f)) p.sc.merge_ok = 0;
   p.recip_s = (float)cd.recip_spp_sqrt;
   p.maxc = (float)cd.max_contribution;
   p.s = cd.spp_sqrt;
@@ -1355,19 +1366,6 @@ static int render_multi(rt_scene* scene, const rt_camera* cam, const rt_render_o
       if (can_b && (rc = enable_peer(d0, devices[i]))) return rc;
     }
   HIP_OK(hipSetDevice(d0));
-  // rt_progress: this call's shares are the tracked render unless another holds it
-  bool track = false;
-  {
-    std::lock_guard<std::mutex> lk(s->prog.mu);
-    if (!s->prog.busy) {
-      track = true;
-      s->prog.total = (uint64_t)H * W * cd.spp_sqrt * cd.spp_sqrt;
-      s->prog.done = 0;
-      s->prog.events.clear();
-      s->prog.cum.clear();
-      s->prog.busy = 1;
-    }
-  }
   // RCCL gather (RT_FLAG_GATHER_RCCL): communicators over the device list, cached
   const bool use_rccl = (o.flags & RT_FLAG_GATHER_RCCL) != 0;
   RcclGather* rg = nullptr;
@@ -1407,6 +1405,33 @@ static int render_multi(rt_scene* scene, const rt_camera* cam, const rt_render_o
     }
     HIP_OK(hipSetDevice(d0));
   }
+  // rt_progress: this call's shares are the tracked render unless another holds it.
+  // Claimed only after every early return of the setup above; the guard is built in
+  // the same statement sequence, so every return below releases it.
+  bool track = false;
+  {
+    std::lock_guard<std::mutex> lk(s->prog.mu);
+    if (!s->prog.busy) {
+      track = true;
+      s->prog.total = (uint64_t)H * W * cd.spp_sqrt * cd.spp_sqrt;
+      s->prog.done = 0;
+      s->prog.device = d0;
+      s->prog.events.clear();  // no slice events: the shares add their samples when done
+      s->prog.cum.clear();
+      s->prog.busy = 1;
+    }
+  }
+  struct ProgressDone {  // every return path below ends the tracked state
+    Progress& p;
+    bool track;
+    bool ok = false;
+    ~ProgressDone() {
+      if (!track) return;
+      std::lock_guard<std::mutex> lk(p.mu);
+      if (ok) p.done = p.total;
+      p.busy = 0;
+    }
+  } prog_done{s->prog, track};
   std::vector<rt_stats> st(n);
   std::vector<int> rcs(n, RT_OK);
   std::vector<std::string> errs(n);
@@ -1423,20 +1448,14 @@ static int render_multi(rt_scene* scene, const rt_camera* cam, const rt_render_o
         rcs[i] = render_impl(scene, cam, &oi, nullptr, rg->send[i], &st[i], 1 + i, nullptr);
       else
         rcs[i] = render_impl(scene, cam, &oi, nullptr, nullptr, &st[i], 1 + i, &g);
-      if (rcs[i] != RT_OK) errs[i] = rt_last_error();
+      if (rcs[i] != RT_OK) {
+        errs[i] = rt_last_error();
+      } else if (track) {  // rt_progress advances share by share
+        std::lock_guard<std::mutex> lk(s->prog.mu);
+        s->prog.done = std::min(s->prog.total, s->prog.done + st[i].samples);
+      }
     });
   for (auto& t : th) t.join();
-  struct ProgressDone {  // every return path below ends the tracked state
-    Progress& p;
-    bool track;
-    bool ok = false;
-    ~ProgressDone() {
-      if (!track) return;
-      std::lock_guard<std::mutex> lk(p.mu);
-      if (ok) p.done = p.total;
-      p.busy = 0;
-    }
-  } prog_done{s->prog, track};
   for (int i = 0; i < n; ++i)
     if (rcs[i] != RT_OK) return set_error(rcs[i], "rt_render_multi share %d: %s", i, errs[i].c_str());
   if (rg && share_floats > 0) {
@@ -1528,7 +1547,7 @@ int rt_progress(const rt_scene* sc, uint64_t* done, uint64_t* total) {
   rt::Progress& p = const_cast<rt_scene*>(sc)->s.prog;
   std::lock_guard<std::mutex> lk(p.mu);
   *total = p.total;
-  *done = p.busy ? 0 : p.done;
+  *done = p.done;  // 0 while a render without slices is in flight; multi shares add theirs
   if (!p.busy || p.events.empty()) return RT_OK;
   if (hipSetDevice(p.device) != hipSuccess) return rt::set_error(RT_ERR_DEVICE, "rt_progress");
   for (size_t i = 0; i < p.events.size(); ++i) {  // slices complete in stream order

@@ -408,8 +408,10 @@ int rt_render_multi_device(rt_scene* s, const rt_camera* cam, const rt_render_op
 /* Progress of the render in flight on scene s (the reference's progress bar,
  * camera.go:106-108 + internal/progress): may be polled from any thread while
  * rt_render blocks in another.  *total = samples of the current (or last)
- * render; *done = samples of the completed slices (opts.progress_slices), and
- * *total once the render returned. */
+ * render; *done = samples of the completed slices (opts.progress_slices), or
+ * for rt_render_multi the samples of the completed shares, and *total once the
+ * render returned.  A render refused before it starts leaves no render in
+ * flight. */
 int rt_progress(const rt_scene* s, uint64_t* done, uint64_t* total);
 
 /* Output: PrintColor vec/color.go:23-46 (NaN->0, sqrt gamma, clamp .99999, x256). */

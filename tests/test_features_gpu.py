@@ -1,19 +1,18 @@
 """Per-feature GPU-vs-oracle parity: one small scene per reference feature.
 
 Tolerance: >= 99.5 % of linear-RGB channels within
-2^-10 * max(1, |ref|) and of 8-bit outputs equal -- or, where the oracle's own fp32
-twin (the reference's algorithm evaluated in float) does not reach 99.5 % against
-its fp64 path on the same pixels, at least the fp32 twin's agreement and >= 99 %
-(tests/parity.py fp32_bar).  Every comparison and its fp32 floor are in the
-committed PARITY_LOG files (profiles/r3_parity_*.jsonl): e.g. `cluster` (200 small
-spheres) 0.9932 against an fp32 floor of 0.9883.
+2^-10 * max(1, |ref|) and of 8-bit outputs equal, for every feature scene except the
+one named exception in tests/parity.py P1_EXCEPTIONS (`cluster`, 200 small spheres:
+8-bit equality >= 0.990, measured 0.9941 fused / 0.9922 wavefront).  The oracle's fp32
+twin (the reference's algorithm evaluated in float) is rendered on the same pixels and
+logged next to the GPU's numbers (PARITY_LOG) for information only; it sets no bar.
 """
 import os
 
 import pytest
 
 from tests import scenes
-from tests.parity import compare, fp32_bar
+from tests.parity import compare, p1_bar
 
 pytestmark = pytest.mark.gpu
 ASSETS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets")
@@ -34,8 +33,8 @@ def test_feature_parity(rt, oracle, gpu, name, mode):
     print(name, mode, m, m32, st["segments"], ost["segments"])
     assert st["samples"] == ost["samples"]
     assert abs(st["segments"] - ost["segments"]) <= 0.01 * ost["segments"] + 10
-    assert m["frac_close"] >= fp32_bar(m32, "frac_close"), (m, m32)
-    assert m["q_equal"] >= fp32_bar(m32, "q_equal"), (m, m32)
+    assert m["frac_close"] >= p1_bar(name, "frac_close"), (m, m32)
+    assert m["q_equal"] >= p1_bar(name, "q_equal"), (m, m32)
 
 
 @pytest.mark.parametrize("tables", [1, 3])

@@ -27,11 +27,13 @@ def reference(ws, L):
     return v
 
 
-def kernel(ws, L, cascade):
+def kernel(ws, L, cascade, merge_ok=True):
+    """merge_ok: DevScene.merge_ok -- every colour, albedo and the background >= 0
+    (rt_render.hip upload_scene / render_impl); with it off every vertex is pushed."""
     stack, pend = [], None
     for w in ws:
         if pend is not None:
-            merge = len(stack) > 0 and np.all(pend >= 0) and np.all(pend <= 1)
+            merge = merge_ok and len(stack) > 0 and np.all(pend >= 0) and np.all(pend <= 1)
             if merge:
                 stack[-1] = stack[-1] * pend
                 while cascade and len(stack) >= 2 and np.all(stack[-1] >= 0) and \
@@ -75,3 +77,26 @@ def test_zero_and_boundary_weights():
         for cascade in (False, True):
             got, _ = kernel(ws, L, cascade)
             np.testing.assert_allclose(got, reference(ws, L), rtol=1e-12, atol=1e-15)
+
+
+def test_negative_radiance_needs_the_unmerged_fold():
+    """A negative background or colour makes the suffix products signed: a weight in
+    [0, 1]^3 can then raise I(P) (P = (10, -9, 0), w = (1, 0, 0): I 1 -> 10), so the
+    merge would skip a clamp the reference applies.  Scenes with any negative value run
+    with merge_ok = 0 (rt_render.hip), and the telescoped fold alone is exact for any
+    sign: the clamp scales are positive, and a vertex with I <= M never clamps."""
+    ws = [np.array([0.1, 1.0, 1.0]), np.array([1.0, 0.0, 0.0]), np.array([1.0, 1.0, 1.0])]
+    L = np.array([10.0, -9.0, 0.0])
+    merged, _ = kernel(ws, L, cascade=False, merge_ok=True)
+    assert not np.allclose(merged, reference(ws, L))  # the case the flag exists for
+    rng = np.random.default_rng(11)
+    for trial in range(4000):
+        n = int(rng.integers(1, 30))
+        ws = [rng.uniform(-0.5, 1.0, 3) * rng.uniform(0.05, 2.0) for _ in range(n)]
+        if trial % 3 == 0:  # non-negative weights, mixed-sign radiance
+            ws = [np.abs(w) for w in ws]
+        L = rng.uniform(-1.0, 1.0, 3) * rng.choice([0.5, 4.0, 15.0])
+        for cascade in (False, True):
+            got, depth = kernel(ws, L, cascade, merge_ok=False)
+            assert depth == max(0, n - 1)
+            np.testing.assert_allclose(got, reference(ws, L), rtol=1e-10, atol=1e-12)

@@ -5,7 +5,7 @@ fixed point), and oracle parity at BASELINE.json's full sizes on a row subsample
 import numpy as np
 import pytest
 
-from tests.parity import compare, fp32_bar
+from tests.parity import compare, p1_bar
 
 pytestmark = pytest.mark.gpu
 
@@ -88,13 +88,14 @@ def test_sample_overflow_is_flagged_not_clamped(rt, oracle, gpu):
 
 FULL = [
     # BASELINE.json configs at full size; the oracle checks every `stride`-th row.
-    # Bar: SURVEY.md §8(c) P1, >= 99.5 % of channels within 2^-10 and 8-bit equal, or --
-    # where the oracle's fp32 twin itself stays below that against its fp64 path on the
-    # same rows -- at least the fp32 twin's agreement and >= 99 % (tests/parity.py
-    # fp32_bar).  Only C5 takes the second form: its paths bounce along the metal knot
-    # and fork between fp32 and fp64 after 2-14 bounces of accumulated rounding
-    # (tools/fork_probe.py, profiles/r3_fork_probe_model_*.jsonl); measured GPU 0.9926 /
-    # fp32 twin 0.9849 (8-bit), profiles/r3_parity_v1.jsonl.
+    # Bar: SURVEY.md §8(c) P1, >= 99.5 % of channels within 2^-10 and 8-bit equal, for
+    # C2, C3 and C4 (measured 0.9968 / 0.9974 / 0.9952 8-bit equal,
+    # profiles/r3_parity_final.jsonl).  C5 is the one named exception (tests/parity.py
+    # P1_EXCEPTIONS: frac_close >= 0.993, q_equal >= 0.990; measured 0.9946 / 0.9927):
+    # its paths bounce along the metal knot and fork between fp32 and fp64 after 2-14
+    # bounces of accumulated rounding (tools/fork_probe.py,
+    # profiles/r3_fork_probe_model_*.jsonl).  The oracle's fp32 twin is logged beside
+    # (PARITY_LOG, label fp32_oracle) for information; it sets no bar.
     ("cornell", 800, 1024, 1.0, 100),   # C2
     ("book1", 1200, 512, 1.5, 160),     # C3 (aspect 1.5 -> 800 rows, 484 spp)
     ("book2", 800, 4096, 1.0, 100),     # C4 (one GPU here; the split is rank-invariant)
@@ -117,8 +118,8 @@ def test_full_size_parity_on_row_subsample(rt, oracle, gpu, name, width, spp, as
                              precision=32)
     m32 = compare(ref32, ref, label="fp32_oracle")
     print(name, m, m32)
-    assert m["frac_close"] >= fp32_bar(m32, "frac_close"), (m, m32)
-    assert m["q_equal"] >= fp32_bar(m32, "q_equal"), (m, m32)
+    assert m["frac_close"] >= p1_bar(name, "frac_close"), (m, m32)
+    assert m["q_equal"] >= p1_bar(name, "q_equal"), (m, m32)
     assert abs(m["mean_gpu"] - m["mean_ref"]) <= 2e-3 * max(1.0, abs(m["mean_ref"]))
     seg_ratio = (st["segments"] / st["samples"]) / (ost["segments"] / ost["samples"])
     assert abs(seg_ratio - 1) < 0.01
@@ -221,8 +222,19 @@ def test_render_multi_rccl_gather(rt, gpu):
         assert np.array_equal(one, a, equal_nan=True)
         assert np.array_equal(one, b, equal_nan=True)
         assert sta["samples"] == st1["samples"]
+        assert sc.progress() == (sta["samples"], sta["samples"])
         with pytest.raises(RuntimeError):
             sc.render_multi(cam, [0, 0], seed=6, rccl=True)
+        # the refused call left no render in flight: progress still reports the last
+        # render as complete, and the next render (another spp) is tracked again
+        assert sc.progress() == (sta["samples"], sta["samples"])
+        cam.SamplesPerPixel = 4
+        _, st4 = sc.render(cam, seed=6)
+        assert st4["samples"] != sta["samples"]
+        assert sc.progress() == (st4["samples"], st4["samples"])
+        _, st4m = sc.render_multi(cam, [0, 0], seed=6)
+        assert sc.progress() == (st4m["samples"], st4m["samples"])
+        cam.SamplesPerPixel = 16
         if n >= 2:
             for devs in ([0, 1], [1, 0]):
                 c, _ = sc.render_multi(cam, devs, seed=6, rccl=True)
