@@ -13,7 +13,8 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from ._lib import (RT_NOISE_MARBLE, RT_NOISE_PERLIN, RT_NOISE_TURBULENT, RtCamera,  # noqa: F401
+from ._lib import (RT_FT_ALL, RT_FT_BOX, RT_NOISE_MARBLE, RT_NOISE_PERLIN,  # noqa: F401
+                   RT_NOISE_TURBULENT, RtCamera,
                    RtCameraDerived, RtError, RtRenderOpts, RtSceneInfo, RtStats, RtTreeView,
                    check, lib)
 

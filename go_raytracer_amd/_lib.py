@@ -27,6 +27,8 @@ RT_FLAG_PROFILE = 1
 RT_FLAG_GATHER_RCCL = 2  # rt_render_multi: one RCCL ncclGather instead of peer copies
 RT_FT_SPHERE, RT_FT_TRI, RT_FT_METAL, RT_FT_DIEL = 1, 2, 4, 8
 RT_FT_MEDIA, RT_FT_CHECKER, RT_FT_IMAGE, RT_FT_NOISE = 16, 32, 64, 128
+RT_FT_BOX = 256
+RT_FT_ALL = 511
 RT_MODE_AUTO, RT_MODE_WAVEFRONT, RT_MODE_FUSED = 0, 1, 2
 
 D3 = C.c_double * 3

@@ -111,6 +111,18 @@ struct Flattener {
   std::vector<F4> lo, hi;
   std::vector<uint32_t> world_refs;
 
+  // Box leaves (rt_device.h "box leaf"): a NewBox in the world becomes one leaf ref of
+  // type PRIM_BOX; its six quads are emitted as usual (same quad indices) but reached
+  // through the box record.  expand_boxes() puts the six face refs back in its place
+  // (small scenes, kernels without FT_BOX): then the scene is exactly the per-quad one.
+  struct BoxLeaf {
+    size_t pos;            // index in world_refs
+    uint32_t face_ref[6];  // in the list's order: front, right, back, left, top, bottom
+    F4 flo[6], fhi[6];     // their padded bounds
+  };
+  std::vector<BoxLeaf> box_leaves;
+  bool box_leaves_on = true;
+
   explicit Flattener(const Tree& tr, HostScene& o) : t(tr), out(o) {
     has_med.assign(t.nodes.size(), -1);
     box_done.assign(t.nodes.size(), 0);
@@ -245,7 +257,7 @@ struct Flattener {
   }
 
   // ------------------------------------------------------------ emission
-  void add_bounds(uint32_t ref, D3 mn, D3 mx) {
+  static void padded_bounds(D3 mn, D3 mx, F4* lp, F4* hp) {
     // conservative fp32 box: round outward, then pad by a relative epsilon
     double ext = std::max({mx.x - mn.x, mx.y - mn.y, mx.z - mn.z, 0.0});
     double m = std::max({fabs(mn.x), fabs(mn.y), fabs(mn.z), fabs(mx.x), fabs(mx.y), fabs(mx.z)});
@@ -258,9 +270,101 @@ struct Flattener {
     h.x = nextafterf(h.x, INFINITY);
     h.y = nextafterf(h.y, INFINITY);
     h.z = nextafterf(h.z, INFINITY);
+    *lp = l;
+    *hp = h;
+  }
+  void add_bounds(uint32_t ref, D3 mn, D3 mx) {
+    F4 l, h;
+    padded_bounds(mn, mx, &l, &h);
     lo.push_back(l);
     hi.push_back(h);
     world_refs.push_back(ref);
+  }
+
+  // The BVH node rt_new_box builds (NewBox objects.go:208-240, host_tree.cpp): six quad
+  // children, exactly front, right, back, left, top, bottom of the box [mn, mx] with the
+  // edge vectors computed as rt_new_box computes them.  Exact comparisons: a user list
+  // that only looks like a box (or a degenerate one) stays six quads.
+  bool is_newbox(const rt_node& n, D3* pmn, D3* pmx) const {
+    if (n.kind != RT_NODE_BVH) return false;
+    const auto& ch = kids(n);
+    if (ch.size() != 6) return false;
+    for (int c : ch)
+      if (t.nodes[c].kind != RT_NODE_QUAD) return false;
+    auto Q = [&](int k) { return mk(t.nodes[ch[k]].p); };
+    auto U = [&](int k) { return mk(t.nodes[ch[k]].p + 3); };
+    auto V = [&](int k) { return mk(t.nodes[ch[k]].p + 6); };
+    const D3 mn = Q(5);
+    const D3 mx = {Q(1).x, Q(4).y, Q(0).z};
+    const double dx = mx.x - mn.x, dy = mx.y - mn.y, dz = mx.z - mn.z;
+    if (!(dx > 0.0 && dy > 0.0 && dz > 0.0)) return false;
+    auto eq = [](D3 a, D3 b) { return a.x == b.x && a.y == b.y && a.z == b.z; };
+    const D3 ex = {dx, 0, 0}, ey = {0, dy, 0}, ez = {0, 0, dz}, nx = {-dx, 0, 0}, nz = {0, 0, -dz};
+    const bool ok = eq(Q(0), D3{mn.x, mn.y, mx.z}) && eq(U(0), ex) && eq(V(0), ey) &&
+                    eq(Q(1), D3{mx.x, mn.y, mx.z}) && eq(U(1), nz) && eq(V(1), ey) &&
+                    eq(Q(2), D3{mx.x, mn.y, mn.z}) && eq(U(2), nx) && eq(V(2), ey) &&
+                    eq(Q(3), mn) && eq(U(3), ez) && eq(V(3), ey) &&
+                    eq(Q(4), D3{mn.x, mx.y, mx.z}) && eq(U(4), ex) && eq(V(4), nz) &&
+                    eq(Q(5), mn) && eq(U(5), ex) && eq(V(5), ez);
+    if (ok) *pmn = mn, *pmx = mx;
+    return ok;
+  }
+
+  // one box leaf: the six faces as quads (in list order, as the per-quad walk would emit
+  // them), the box record and one world ref over their union
+  void emit_box(const rt_node& n, const Xf& xf, D3 mn, D3 mx) {
+    const auto& ch = kids(n);
+    BoxLeaf bl{};
+    bl.pos = world_refs.size();
+    D3 bmn = {INFINITY, INFINITY, INFINITY}, bmx = {-INFINITY, -INFINITY, -INFINITY};
+    for (int k = 0; k < 6; ++k) {
+      D3 a, b;
+      bl.face_ref[k] = emit_quad(t.nodes[ch[k]], xf, &a, &b);
+      padded_bounds(a, b, &bl.flo[k], &bl.fhi[k]);
+      bmn = {std::min(bmn.x, a.x), std::min(bmn.y, a.y), std::min(bmn.z, a.z)};
+      bmx = {std::max(bmx.x, b.x), std::max(bmx.y, b.y), std::max(bmx.z, b.z)};
+    }
+    // frame: C = the min corner, A / B = the x / z edges (horizontal: rotations are about y)
+    const D3 C = xf.pt(mn), A = xf.rot(D3{mx.x - mn.x, 0, 0}), B = xf.rot(D3{0, 0, mx.z - mn.z});
+    const double a2 = A.x * A.x + A.z * A.z, b2 = B.x * B.x + B.z * B.z;
+    // face slots by plane: x' = 0 left, x' = 1 right, y = lo bottom, y = hi top,
+    // z' = 0 back, z' = 1 front
+    const uint32_t* f = bl.face_ref;
+    const uint32_t slot[6] = {f[3], f[1], f[5], f[4], f[2], f[0]};
+    const uint32_t idx = (uint32_t)(out.box_recs.size() / 4);
+    out.box_recs.push_back({(float)C.x, (float)C.z, (float)C.y, 0.0f});  // .w: the ref (make_record)
+    out.box_recs.push_back({(float)(A.x / a2), (float)(A.z / a2), (float)(B.x / b2), (float)(B.z / b2)});
+    out.box_recs.push_back({(float)xf.pt(mx).y, as_f(slot[0]), as_f(slot[1]), as_f(slot[2])});
+    out.box_recs.push_back({as_f(slot[3]), as_f(slot[4]), as_f(slot[5]), 0.0f});
+    box_leaves.push_back(bl);
+    add_bounds(prim_ref(PRIM_BOX, idx), bmn, bmx);
+  }
+
+  // every box leaf back to its six face refs, in place (world order as without boxes)
+  void expand_boxes() {
+    if (box_leaves.empty()) return;
+    std::vector<F4> nlo, nhi;
+    std::vector<uint32_t> nrefs;
+    size_t b = 0;
+    for (size_t i = 0; i < world_refs.size(); ++i) {
+      if (b < box_leaves.size() && box_leaves[b].pos == i) {
+        for (int k = 0; k < 6; ++k) {
+          nrefs.push_back(box_leaves[b].face_ref[k]);
+          nlo.push_back(box_leaves[b].flo[k]);
+          nhi.push_back(box_leaves[b].fhi[k]);
+        }
+        ++b;
+      } else {
+        nrefs.push_back(world_refs[i]);
+        nlo.push_back(lo[i]);
+        nhi.push_back(hi[i]);
+      }
+    }
+    world_refs.swap(nrefs);
+    lo.swap(nlo);
+    hi.swap(nhi);
+    box_leaves.clear();
+    out.box_recs.clear();
   }
 
   static uint32_t fbits(int32_t v) {
@@ -372,6 +476,11 @@ struct Flattener {
         return RT_OK;
       case RT_NODE_BVH: {
         const auto& ch = kids(n);
+        D3 bmn, bmx;
+        if (role == 0 && box_leaves_on && is_newbox(n, &bmn, &bmx)) {
+          emit_box(n, xf, bmn, bmx);
+          return RT_OK;
+        }
         if (role == 0 && subtree_has_medium(id)) {
           std::vector<int32_t> objs(ch.begin(), ch.end()), pos(ch.size());
           for (size_t i = 0; i < ch.size(); ++i) pos[i] = (int32_t)i;
@@ -460,6 +569,8 @@ int flatten_scene(const Tree& t, int world, int lights, HostScene& out) {
   const bool timing = getenv("RT_TIMING") != nullptr;
   auto t0 = std::chrono::steady_clock::now();
   Flattener f(t, out);
+  const char* bl = getenv("RT_BOX_LEAVES");
+  f.box_leaves_on = !(bl && *bl && atoi(bl) == 0);
   int rc = f.walk(world, Xf{}, 1, 0);
   if (timing)
     fprintf(stderr, "[rt] flatten walk %.3f s\n",
@@ -469,7 +580,6 @@ int flatten_scene(const Tree& t, int world, int lights, HostScene& out) {
     rc = f.walk_lights(lights, 1, 0, 1.0, 0);
     if (rc) return rc;
   }
-  out.n_world_prims = (int32_t)f.world_refs.size();
   // materials / textures / images / perlin tables: indices kept identical to the tree
   for (const auto& m : t.materials) {
     DevMaterial d{};
@@ -505,6 +615,19 @@ int flatten_scene(const Tree& t, int world, int lights, HostScene& out) {
       for (int i = 0; i < 256; ++i) d.perm[a][i] = (uint8_t)p.perm[a][i];
     out.perlins.push_back(d);
   }
+  // Box leaves stay only in large scenes (a tree read through L1/L2: the record loop
+  // and the LDS trees of small scenes test quads) whose kernel set has FT_BOX anyway,
+  // so they never move a scene to a bigger kernel (DESIGN.md §4 "Box leaves").
+  if (!f.box_leaves.empty()) {
+    out.refs = f.world_refs;  // features as they would be with the faces as quads
+    bool nt0 = true;
+    const uint32_t feats = scene_features(out, &nt0) & ~FT_BOX;
+    out.refs.clear();
+    const size_t n_faces = f.world_refs.size() + 5 * f.box_leaves.size();
+    const uint32_t set = (feats & FT_NOISE) && !nt0 ? FT_ALL : pick_ft_set(feats);
+    if (n_faces <= kBoxLeafMinPrims || !(set & FT_BOX)) f.expand_boxes();
+  }
+  out.n_world_prims = (int32_t)f.world_refs.size();
   // keep prim bounds for export, in the BVH's final ref order (set by build_bvh)
   t0 = std::chrono::steady_clock::now();
   // large scenes: PLOC on the GPU (rt_build.hip) when a device is present

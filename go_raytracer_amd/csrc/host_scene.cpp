@@ -43,7 +43,20 @@ uint32_t scene_features(const HostScene& h, bool* noise_table0) {
       f |= FT_MEDIA;
     }
   };
-  for (uint32_t r : h.refs) prim(r);
+  for (uint32_t r : h.refs) {
+    if (r != PRIM_NONE && (r >> 30) == PRIM_BOX) {  // a box leaf: its six face quads
+      f |= FT_BOX;
+      const F4* b = &h.box_recs[4 * (size_t)(r & 0x3FFFFFFFu)];
+      const float fr[6] = {b[2].y, b[2].z, b[2].w, b[3].x, b[3].y, b[3].z};
+      for (float x : fr) {
+        uint32_t q;
+        memcpy(&q, &x, 4);
+        prim(q);
+      }
+      continue;
+    }
+    prim(r);
+  }
   for (uint32_t r : h.medium_refs) prim(r);
   for (const DevLight& l : h.lights) prim(l.ref);
   if (!h.media.empty()) f |= FT_MEDIA;

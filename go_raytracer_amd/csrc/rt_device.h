@@ -20,6 +20,9 @@ struct alignas(8) F2 {
 // ---- primitive references ------------------------------------------------
 // prim ref = (type << 30) | index
 enum : uint32_t { PRIM_SPHERE = 0u, PRIM_QUAD = 1u, PRIM_TRI = 2u, PRIM_MEDIUM = 3u };
+// Type 3 in a WORLD ref / leaf record is a box leaf (media are never BVH leaves: the
+// flattener keeps them apart, so the code is free there).  See "box leaf" below.
+constexpr uint32_t PRIM_BOX = 3u;
 constexpr uint32_t PRIM_NONE = 0xFFFFFFFFu;
 inline constexpr uint32_t prim_ref(uint32_t type, uint32_t idx) { return (type << 30) | idx; }
 
@@ -63,6 +66,13 @@ enum : uint32_t { TRI_HAS_NORMALS = 1u, TRI_HAS_UV = 2u };
 //          (alpha = w.(p x v) = p.A, beta = w.(u x p) = p.B: the triple products of
 //           quad.Hit objects.go:186-187 with the cross products hoisted)
 //  tri:    v0.xyz | ref       ;  e0.xyz | 0           ; e1.xyz | 0 ; 0
+//  box:    C.x C.z ylo | ref  ;  a.x a.z b.x b.z      ; yhi face0 face1 face2 ; face3 face4 face5 0
+//          (a NewBox objects.go:208-240 under RotateY/Translate, large scenes only:
+//           C = its min corner in world space, a = A / |A|^2 and b = B / |B|^2 for its
+//           horizontal edges A (x) and B (z), so x' = (p - C).a and z' = (p - C).b
+//           are the box-frame coordinates in [0, 1]; faces are the six quad refs by
+//           plane: x' = 0, x' = 1, y = ylo, y = yhi, z' = 0, z' = 1.  One slab test
+//           replaces a subtree of six single-quad leaves: rt_kernels.h hit_box_rec)
 // Record-loop pair layout (quad-only scenes of <= kBruteMax prims, largest area
 // first): records 2p and 2p+1 share 128 B, every field as an adjacent (rec 2p,
 // rec 2p+1) float pair so one packed-fp32 op works on both:
@@ -77,8 +87,26 @@ enum : uint32_t {
   FT_SPHERE = 1u, FT_TRI = 2u, FT_METAL = 4u, FT_DIEL = 8u,
   FT_MEDIA = 16u,   // constant media or isotropic materials
   FT_CHECKER = 32u, FT_IMAGE = 64u, FT_NOISE = 128u,
-  FT_ALL = 255u
+  FT_BOX = 256u,    // box leaves in the world BVH (host_flatten.cpp: large scenes only)
+  FT_ALL = 511u
 };
+// the book2 feature set (C4): spheres, media, textures and box leaves
+constexpr uint32_t FT_SET_BOOK2 =
+    FT_SPHERE | FT_METAL | FT_DIEL | FT_MEDIA | FT_IMAGE | FT_NOISE | FT_BOX;
+// Feature sets with a compiled fused kernel, smallest first; a scene runs the first
+// set that covers its features (scene_features).
+constexpr uint32_t kFtSets[] = {
+    0u,                                                     // Cornell box: quads, Lambertian, light
+    FT_MEDIA,                                               // + constant media (Cornell smoke)
+    FT_SPHERE | FT_TRI | FT_METAL,                          // meshes, spheres, Lambertian + metal
+    FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER,   // meshes and spheres, plain materials
+    FT_SET_BOOK2,                                           // spheres, media, textures, boxes
+    FT_ALL};
+inline uint32_t pick_ft_set(uint32_t feats) {
+  for (uint32_t m : kFtSets)
+    if ((feats & ~m) == 0u) return m;
+  return FT_ALL;
+}
 
 struct DevMedium {           // constantMedium medium.go:13-18
   uint32_t bfirst, bcount;   // boundary prim refs in medium_refs

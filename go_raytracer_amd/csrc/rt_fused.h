@@ -68,7 +68,7 @@ constexpr int fused_waves(uint32_t ft, int tree = 4) {
          : ft == FT_MEDIA ? 4
          : ft == (FT_SPHERE | FT_TRI | FT_METAL) ? TRI_WAVES
          : ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? MESH_WAVES
-         : ft == (FT_SPHERE | FT_METAL | FT_DIEL | FT_MEDIA | FT_IMAGE | FT_NOISE) ? FT_TEX_WAVES
+         : ft == FT_SET_BOOK2 ? FT_TEX_WAVES
                                                                                   : 3;
 }
 // LDS clamp-weight entries (12 B each): 6 (C2 +1 %, C3 +2.5 % over 3-4), 4 for the
@@ -106,7 +106,7 @@ constexpr int fused_wlds(uint32_t ft, int tree = 4) {
          : (ft == 0u && tree != 0)                                  ? 4
          : (ft == 0u && tree == 0)                                  ? BRUTE_WLDS
          : ft == FT_ALL                                             ? ALL_WLDS
-         : ft == (FT_SPHERE | FT_METAL | FT_DIEL | FT_MEDIA | FT_IMAGE | FT_NOISE) ? TEX_WLDS
+         : ft == FT_SET_BOOK2 ? TEX_WLDS
                                                                     : kLdsWMax;
 }
 // short traversal stack: none for the record loop, 6 entries for the lean set
@@ -116,7 +116,7 @@ constexpr int fused_short(uint32_t ft, int tree = 4) {
          : ft == 0u                                                   ? kShortStackMin
          : ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? MESH_SHORT
          : ft == (FT_SPHERE | FT_TRI | FT_METAL)                      ? TRI_SHORT
-         : ft == (FT_SPHERE | FT_METAL | FT_DIEL | FT_MEDIA | FT_IMAGE | FT_NOISE) ? TEX_SHORT
+         : ft == FT_SET_BOOK2 ? TEX_SHORT
                                                                       : kShortStack;
 }
 // + 24 B per lane of chunk sums (SampleAcc) + the perlin tables of noise kernels
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
   Trav tr;
   tr.cur = TRAV_DONE;
   bool has = false;
-  WaveBatch b = {};
+  WaveBatch b = batch_init(P);
   const unsigned long long t_start = P.wave_times ? wall_clock64() : 0ull;
   // Scheduling round: lanes without work take a chunk; traversing lanes run up
   // to step_budget traversal steps; lanes whose traversal is done are shaded
@@ -163,8 +163,7 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
   PH_T(t_loop);
   for (;;) {
     PH_T(t_grab);
-    const uint32_t c =
-        grab_chunk<FT != (FT_SPHERE | FT_METAL | FT_DIEL | FT_MEDIA | FT_IMAGE | FT_NOISE)>(P, b, !has);
+    const uint32_t c = grab_chunk(P, b, !has);
     if (c != 0xFFFFFFFFu) {
       start_sample<false, cam_mode(FT)>(P, slot, s, c, 0);
       trav_init(P.sc, s.d, tr);

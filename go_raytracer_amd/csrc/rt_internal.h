@@ -46,6 +46,7 @@ struct HostScene {
   std::vector<F4> quad;      // 5 per quad
   std::vector<F4> tri;       // 3 per tri
   std::vector<F4> tri_attr;  // 6 per tri
+  std::vector<F4> box_recs;  // 4 per box leaf: the leaf record (rt_device.h), ref in [0].w
   std::vector<F4> nodes;     // BVH2, 4 per node (export / structural tests)
   std::vector<F4> nodes4;    // BVH4 the kernels traverse, 8 per node (rt_device.h)
   uint32_t root4 = PRIM_NONE;
@@ -131,6 +132,8 @@ int build_bvh8(HostScene& s);
 int build_bvh_device(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi,
                      const std::vector<uint32_t>& prims, int device);
 bool bvh_device_available();
+// box leaves only in scenes of more world prims than this (counting faces; host_flatten.cpp)
+constexpr size_t kBoxLeafMinPrims = 256;
 // host_scene.cpp: RT_FT_* features a flattened scene needs
 uint32_t scene_features(const HostScene& h, bool* noise_table0 = nullptr);
 // rt_render.hip

@@ -316,12 +316,56 @@ RT_D bool hit_tri_rec(const F4 r[4], f3 o, f3 d, float tmin, float tmax, float& 
   v_out = v;
   return true;
 }
+// A box leaf (rt_device.h "box leaf"): NewBox's six quads (objects.go:208-240, closed
+// intervals like quad.Hit :167-196) as one slab test in the box's frame, the frame of
+// rotateY.Hit (transformation.go:94-107): x' = (o - C).a + t d.a, z' likewise, y as is;
+// the faces are the planes x' = 0 / 1, y = ylo / yhi, z' = 0 / 1.  The closest face with
+// t in [tmin, tmax] is the entering one when t_near >= tmin, else the leaving one (a ray
+// that starts inside).  ref = that face's quad ref; u = -1 marks (alpha, beta) as not
+// computed: shade_core derives them from the face's quad record when its material reads
+// them (only image textures do).  iy = 1 / d.y (the traversal's).
+RT_D bool hit_box_rec(const F4 r[4], f3 o, f3 d, float iy, float tmin, float tmax, float& t_out,
+                      uint32_t& ref) {
+  const float ex = o.x - r[0].x, ez = o.z - r[0].y;
+  const float lx = fmaf(ez, r[1].y, ex * r[1].x), lz = fmaf(ez, r[1].w, ex * r[1].z);
+  const float ix = rcp(fmaf(d.z, r[1].y, d.x * r[1].x)), iz = rcp(fmaf(d.z, r[1].w, d.x * r[1].z));
+  // (1 - l) * i, not fma(-l, i, i): a ray parallel to the slab (i = inf) inside it
+  // must get +-inf for both planes, not -inf + inf = NaN
+  const float tx0 = -lx * ix, tx1 = (1.0f - lx) * ix;
+  const float tz0 = -lz * iz, tz1 = (1.0f - lz) * iz;
+  const float ty0 = (r[0].z - o.y) * iy, ty1 = (r[2].x - o.y) * iy;
+  const float nx = fminf(tx0, tx1), ny = fminf(ty0, ty1), nz = fminf(tz0, tz1);
+  const float fx = fmaxf(tx0, tx1), fy = fmaxf(ty0, ty1), fz = fmaxf(tz0, tz1);
+  const float tn = fmaxf(fmaxf(nx, ny), nz), tf = fminf(fminf(fx, fy), fz);
+  const bool enter = tn >= tmin;
+  const float t = enter ? tn : tf;
+  if (!(tn <= tf && t >= tmin && t <= tmax)) return false;
+  // the face: the slab whose plane gave t, and which of its two planes
+  int slot;
+  if (enter)
+    slot = tn == nx ? (tx1 < tx0 ? 1 : 0) : tn == ny ? (ty1 < ty0 ? 3 : 2) : (tz1 < tz0 ? 5 : 4);
+  else
+    slot = tf == fx ? (tx1 > tx0 ? 1 : 0) : tf == fy ? (ty1 > ty0 ? 3 : 2) : (tz1 > tz0 ? 5 : 4);
+  const float fr[6] = {r[2].y, r[2].z, r[2].w, r[3].x, r[3].y, r[3].z};
+  float f = fr[0];
+#pragma unroll
+  for (int k = 1; k < 6; ++k) f = slot == k ? fr[k] : f;
+  ref = fbits(f);
+  t_out = t;
+  return true;
+}
+
 #define HAS(f) ((FT & (f)) != 0u)
 template <uint32_t FT>
-RT_D bool hit_record(const F4 r[4], f3 o, f3 d, float time, float tmin, float tmax, float& t,
-                     float& u, float& v, uint32_t& ref) {
+RT_D bool hit_record(const F4 r[4], f3 o, f3 d, float iy, float time, float tmin, float tmax,
+                     float& t, float& u, float& v, uint32_t& ref) {
   ref = fbits(r[0].w);
   const uint32_t type = ref >> 30;
+  if (HAS(FT_BOX) && type == PRIM_BOX) {
+    u = -1.0f;  // (alpha, beta) deferred to shade_core
+    v = 0.0f;
+    return hit_box_rec(r, o, d, iy, tmin, tmax, t, ref);
+  }
   if (!HAS(FT_SPHERE | FT_TRI) || type == PRIM_QUAD) return hit_quad_rec(r, o, d, tmin, tmax, t, u, v);
   if (HAS(FT_TRI) && (!HAS(FT_SPHERE) || type == PRIM_TRI))
     return hit_tri_rec(r, o, d, tmin, tmax, t, u, v);

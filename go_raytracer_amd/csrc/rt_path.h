@@ -17,6 +17,8 @@ constexpr int kShortStackMin = 6;  // smallest short stack of any kernel (fused 
 constexpr int kBruteMax = 48;      // scenes up to this many leaf entries skip the tree (fused)
 constexpr int kMaxIt = 1 << 16;  // per-iteration counter slots (no per-iteration memsets)
 constexpr int kXcd = 8;          // queue counters are sharded per XCD (blockIdx % 8)
+constexpr int kMaxParts = 64;    // chunk-range partitions of the fused kernel (one counter each)
+constexpr int kPartStride = 64;  // u32 between partition counters (256 B: own cache lines)
 
 enum : uint32_t { F_PEND = 1u, F_PRE = 2u, F_NONFINITE = 4u };
 enum { OUT_DEAD = 0, OUT_ALIVE = 1, OUT_NEED_CHUNK = 2 };
@@ -27,6 +29,7 @@ struct Counters {
   unsigned long long overflow;  // samples whose channel left the fixed-point range (add_sample)
   uint32_t chunk_head;
   uint32_t _pad[11];
+  uint32_t part[kMaxParts * kPartStride];  // fused kernel: next position of partition p at [p * stride]
   uint32_t cnt[kMaxIt][kXcd];  // per-XCD queue lengths entering iteration i
 };
 
@@ -59,6 +62,8 @@ struct Params {
   int step_budget;     // fused: traversal steps per scheduling round
   uint32_t shade_min;  // fused: lanes that must be waiting before a wave shades
   uint32_t grab_min;   // fused: chunks a wave takes per refill of its batch (>= 1)
+  uint32_t parts_log2; // fused: the chunk range is split over 2^parts_log2 partitions ...
+  uint32_t gran_log2;  // ... interleaved in granules of 2^gran_log2 chunks (grab_chunk)
   unsigned long long* wave_times;  // debug (RT_WAVE_TIMES): per wave {start, end, segments}
   uint32_t recs_lds;   // leaf records cached in LDS after the nodes (stage_nodes)
   uint64_t seed;
@@ -194,7 +199,7 @@ __shared__ F4 g_cam[6];
 // kernels lost from it (their VGPR budget takes the loaded constants: C2 +26 %)
 constexpr bool cam_lds(uint32_t ft) {
   return ft == (FT_SPHERE | FT_TRI | FT_METAL) ||
-         ft == (FT_SPHERE | FT_METAL | FT_DIEL | FT_MEDIA | FT_IMAGE | FT_NOISE);
+         ft == FT_SET_BOOK2;
 }
 // Where a kernel reads the camera constants: 1 = g_cam (book2 set), 2 = scalar loads from
 // the kernel-argument segment where a ray starts (kparams: SGPRs live only there), 0 = the
@@ -206,7 +211,7 @@ constexpr int cam_mode(uint32_t ft) {
 #ifdef RT_CAM_SGPR
   return cam_lds(ft) ? 1 : 0;
 #else
-  return ft == (FT_SPHERE | FT_METAL | FT_DIEL | FT_MEDIA | FT_IMAGE | FT_NOISE) ? 1 : 2;
+  return ft == FT_SET_BOOK2 ? 1 : 2;
 #endif
 }
 typedef __attribute__((address_space(4))) const Params cst_params;
@@ -467,7 +472,7 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
         for (uint32_t k = 0;;) {
           float t, u, vv;
           uint32_t ref;
-          if (hit_record<FT>(rec, o, d, time, tmin, tr.best.t, t, u, vv, ref)) {
+          if (hit_record<FT>(rec, o, d, inv.y, time, tmin, tr.best.t, t, u, vv, ref)) {
             tr.best.t = t;
             tr.best.u = u;
             tr.best.v = vv;
@@ -563,7 +568,7 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
         }
         float t, u, v;
         uint32_t ref;
-        if (hit_record<FT>(rec, o, d, time, tmin, tr.best.t, t, u, v, ref)) {
+        if (hit_record<FT>(rec, o, d, inv.y, time, tmin, tr.best.t, t, u, v, ref)) {
           tr.best.t = t;
           tr.best.u = u;
           tr.best.v = v;
@@ -687,7 +692,7 @@ RT_D int trav_steps8(const DevScene& sc, const TravStack& stack, f3 o, f3 d, flo
       for (uint32_t k = 0;;) {
         float t, u, vv;
         uint32_t ref;
-        if (hit_record<FT>(rec, o, d, time, tmin, tr.best.t, t, u, vv, ref)) {
+        if (hit_record<FT>(rec, o, d, inv.y, time, tmin, tr.best.t, t, u, vv, ref)) {
           tr.best.t = t;
           tr.best.u = u;
           tr.best.v = vv;
@@ -1597,6 +1602,17 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
       mat = (int)fbits(q[2].w);
       ff = dot(d, nout) < 0;
       n = ff ? nout : -nout;
+      if (HAS(FT_BOX) && u < 0.0f) {
+        // a box leaf's face (hit_box_rec): quad.Hit's alpha, beta (objects.go:186-187) at
+        // this p, computed only when the material reads them (image textures)
+        if (HAS(FT_IMAGE) && sc.mats[mat]._pad != 0.0f) {
+          const f3 pp = p - xyz(q[0]), w = xyz(q[4]);
+          u = dot(w, cross(pp, xyz(q[2])));
+          v = dot(w, cross(xyz(q[1]), pp));
+        } else {
+          u = v = 0.0f;
+        }
+      }
     } else if (HAS(FT_TRI) && (!HAS(FT_MEDIA) || type == PRIM_TRI)) {
       nout = tri_normal(sc, idx, u, v);
       mat = (int)fbits(sc.tri[3 * (size_t)idx].w);
@@ -1723,7 +1739,9 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
           // Needs P_k+1 >= 0 in every channel: scenes with a negative colour, albedo or
           // background (sc.merge_ok = 0) push every vertex, which the fold handles exactly
           // for any sign.
-          const bool merge = sc.merge_ok && s.nst > 0 && pv.x >= 0.0f && pv.y >= 0.0f &&
+          // (the flag is re-read from the kernel-argument segment here, kparams(): held in
+          // an SGPR across the loop it added SGPR spills)
+          const bool merge = kparams()->sc.merge_ok && s.nst > 0 && pv.x >= 0.0f && pv.y >= 0.0f &&
                              pv.z >= 0.0f && pv.x <= 1.0f && pv.y <= 1.0f && pv.z <= 1.0f;
 #else
           const bool merge = false;
@@ -1813,50 +1831,93 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
   return OUT_NEED_CHUNK;
 }
 
-// Wave-batched work distribution: lanes that need a chunk take consecutive ids
-// from the wave's current batch; the batch is refilled with ONE returning
-// atomic per >= grab_min chunks (a single counter saturates near 88 returning
-// atomics per µs on MI355X, so per-event atomics would serialise the whole chip;
-// 8-GPU share of C2: 41 ms with 1-chunk grabs, 8.0 ms with 64).  Splitting the
-// range over 8 partition counters measured 6-12 % slower (C2, 1 and 8 ranks).
+// Wave-batched work distribution over partitioned counters.  The chunk range is split
+// into NP = 2^parts_log2 partitions, interleaved in granules of G = 2^gran_log2 chunks
+// (granule j belongs to partition j % NP), each with its own counter of positions
+// (Counters::part, 256 B apart).  Every partition therefore sweeps the image in the same
+// order as one counter would (the row-group locality of chunk_pixel is kept), while the
+// returning atomics are spread over NP addresses: one address saturates near 88
+// returning atomics per µs on MI355X, which is what forced large batches (and the long
+// tail they leave when the range runs out) on a single counter.  A wave starts on
+// partition (wave id % NP); when its partition is used up it probes every counter with
+// one load per lane and moves to the next one with work left.  Partitions whose atomic
+// came back exhausted are remembered (`dead`), so the search ends after at most NP + 1
+// atomics even on stale probes.  Lanes that need a chunk take consecutive positions from
+// the wave's batch; the batch is refilled with ONE returning atomic per >= grab_min
+// positions.  parts_log2 = 0 is the single counter (progress slices use it).
 struct WaveBatch {
-  uint32_t next, end;  // wave-uniform
+  uint32_t next, end;   // wave-uniform: positions [next, end) of partition `part`
+  uint32_t part;        // the wave's partition; kMaxParts once every partition is used up
+  unsigned long long dead;  // partitions known exhausted
 };
-// SGB: the leader's atomic result read into an SGPR (v_readlane, no LDS permute) and the
-// batch bounds kept wave-uniform in SGPRs instead of VGPRs: C2 -0.6 % (its 4 spilled VGPRs
-// gone), C5 -1.6 %, C3 -0.1 %, but C4 +0.8 % (r3_batch_sgpr_ab.jsonl; bit-identical)
-template <bool SGB>
+RT_D uint32_t part_end(const Params& P, uint32_t p) {
+  const uint32_t gl = P.gran_log2, lg = P.parts_log2;
+  const uint32_t granules = (P.n_chunks + (1u << gl) - 1u) >> gl;
+  return granules > p ? (((granules - p - 1u) >> lg) + 1u) << gl : 0u;
+}
+RT_D uint32_t part_chunk(const Params& P, uint32_t p, uint32_t pos) {
+  const uint32_t gl = P.gran_log2;
+  return ((((pos >> gl) << P.parts_log2) + p) << gl) | (pos & ((1u << gl) - 1u));
+}
+RT_D WaveBatch batch_init(const Params& P) {
+  const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  return {0u, 0u, wave & ((1u << P.parts_log2) - 1u), 0ull};
+}
 RT_D uint32_t grab_chunk(const Params& P, WaveBatch& b, bool need) {
   const unsigned long long m = __ballot(need);
   if (!m) return 0xFFFFFFFFu;
   const uint32_t n = (uint32_t)__popcll(m);
   const uint32_t r = prefix_count(m);
   const uint32_t avail = b.end - b.next;
-  uint32_t mine;
+  uint32_t pos, part;
   if (n <= avail) {
-    mine = b.next + r;
-    if (SGB) b.next = __builtin_amdgcn_readfirstlane(b.next + n);
-    else b.next += n;
+    pos = b.next + r;
+    part = b.part;
+    b.next = __builtin_amdgcn_readfirstlane(b.next + n);
   } else {
-    // (smaller batches over the last part of the range measured 4-15 % slower,
-    // even over its last 0.5 %: profiles/r1_wave_timeline.jsonl, r1_tail_sweep.jsonl)
-    const uint32_t grab = max(P.grab_min, n - avail);
-    uint32_t g = 0;
-    if (lane_id() == (uint32_t)(__ffsll((long long)m) - 1)) g = atomicAdd(&P.ctr->chunk_head, grab);
-    if (SGB) {
-      g = __builtin_amdgcn_readlane(g, __ffsll((long long)m) - 1);
-      mine = r < avail ? b.next + r : g + (r - avail);
-      b.next = __builtin_amdgcn_readfirstlane(g + (n - avail));
-      b.end = __builtin_amdgcn_readfirstlane(g + grab);
-    } else {
-      g = __shfl(g, __ffsll((long long)m) - 1);
-      mine = r < avail ? b.next + r : g + (r - avail);
-      b.next = g + (n - avail);
-      b.end = g + grab;
+    const uint32_t old_next = b.next, old_part = b.part;
+    const uint32_t leader = (uint32_t)(__ffsll((long long)m) - 1);
+    const uint32_t np = 1u << P.parts_log2;
+    uint32_t g = 0u, gend = 0u;
+    // a wave-uniform loop: each pass either takes a batch, finds every partition used
+    // up, or marks one more partition dead (at most NP + 1 passes)
+    while (b.part < (uint32_t)kMaxParts) {
+      const uint32_t endp = part_end(P, b.part);
+      const uint32_t want = max(P.grab_min, n - avail);
+      uint32_t v = 0u;
+      if (lane_id() == leader) v = atomicAdd(&P.ctr->part[b.part * kPartStride], want);
+      g = __builtin_amdgcn_readlane(v, leader);
+      if (g < endp) {
+        gend = min(g + want, endp);
+        break;
+      }
+      b.dead |= 1ull << b.part;
+      // probe: lane i reads partition i's counter (stale values only read low)
+      const uint32_t li = lane_id();
+      bool left = false;
+      if (li < np)
+        left = __hip_atomic_load(&P.ctr->part[li * kPartStride], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT) < part_end(P, li);
+      const unsigned long long live = __ballot(left) & ~b.dead;
+      if (!live) {
+        b.part = (uint32_t)kMaxParts;
+        break;
+      }
+      // the next live partition after this one, cyclically
+      const uint32_t sh = b.part + 1u;
+      const unsigned long long rot = sh >= 64u ? live : ((live >> sh) | (live << (64u - sh)));
+      b.part = __builtin_amdgcn_readfirstlane((sh + (uint32_t)(__ffsll((long long)rot) - 1)) & 63u);
     }
+    const uint32_t take = r - avail;  // this lane's offset in the new batch (r >= avail)
+    pos = r < avail ? old_next + r : g + take;
+    part = r < avail ? old_part : b.part;
+    if (r >= avail && (b.part >= (uint32_t)kMaxParts || g + take >= gend)) part = (uint32_t)kMaxParts;
+    b.next = __builtin_amdgcn_readfirstlane(min(g + (n - avail), gend));
+    b.end = __builtin_amdgcn_readfirstlane(gend);
   }
-  if (!need) return 0xFFFFFFFFu;
-  return mine < P.n_chunks ? mine : 0xFFFFFFFFu;
+  if (!need || part >= (uint32_t)kMaxParts) return 0xFFFFFFFFu;
+  const uint32_t c = part_chunk(P, part, pos);
+  return c < P.n_chunks ? c : 0xFFFFFFFFu;
 }
 
 }  // namespace rt

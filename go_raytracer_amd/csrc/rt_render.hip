@@ -348,6 +348,9 @@ static void make_record(const HostScene& h, uint32_t ref, F4* r) {
       const F4 cr = h.sph_cr[idx], mv = h.sph_mv[idx];
       r[0] = {cr.x, cr.y, cr.z, rb};
       r[1] = {mv.x, mv.y, mv.z, cr.w};
+    } else if (type == PRIM_BOX) {  // box leaf (rt_device.h), built by the flattener
+      for (int k = 0; k < 4; ++k) r[k] = h.box_recs[4 * (size_t)idx + k];
+      r[0].w = rb;
     } else if (type == PRIM_QUAD) {
       const F4* q = &h.quad[5 * (size_t)idx];  // Q|D, u|area, v|mat, n, w
       const double u[3] = {q[1].x, q[1].y, q[1].z}, v[3] = {q[2].x, q[2].y, q[2].z},
@@ -755,18 +758,9 @@ static int occupancy_blocks(const void* kernel, int device, int* out, size_t dyn
   return RT_OK;
 }
 
-// Feature sets with a compiled fused kernel, smallest first; a scene runs the
-// first set that covers its features (scene_features).
-static constexpr uint32_t kFtSets[] = {
-    0u,                                                     // Cornell box: quads, Lambertian, light
-    FT_MEDIA,                                               // + constant media (Cornell smoke)
-    FT_SPHERE | FT_TRI | FT_METAL,                          // meshes, spheres, Lambertian + metal
-    FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER,   // meshes and spheres, plain materials
-    FT_SPHERE | FT_METAL | FT_DIEL | FT_MEDIA | FT_IMAGE | FT_NOISE,  // spheres, media, textures
-    FT_ALL};
 static_assert(FT_SPHERE == RT_FT_SPHERE && FT_TRI == RT_FT_TRI && FT_METAL == RT_FT_METAL &&
                   FT_DIEL == RT_FT_DIEL && FT_MEDIA == RT_FT_MEDIA && FT_CHECKER == RT_FT_CHECKER &&
-                  FT_IMAGE == RT_FT_IMAGE && FT_NOISE == RT_FT_NOISE,
+                  FT_IMAGE == RT_FT_IMAGE && FT_NOISE == RT_FT_NOISE && FT_BOX == RT_FT_BOX,
               "feature bits: rt_device.h and rt_abi.h disagree");
 
 #define RT_FUSED_EXTERN(L, F, T) extern template __global__ void k_fused<L, F, T>(Params);
@@ -784,11 +778,7 @@ static const void* fused_for(uint32_t set) {
     default: return (const void*)k_fused<LDS, FT_ALL, 4>;
   }
 }
-static uint32_t pick_set(uint32_t feats) {
-  for (uint32_t m : kFtSets)
-    if ((feats & ~m) == 0u) return m;
-  return FT_ALL;
-}
+static uint32_t pick_set(uint32_t feats) { return pick_ft_set(feats); }
 // BVH2 kernels exist for the two smallest sets with the tree in LDS (tiny scenes)
 static const void* pick_fused(bool lds, uint32_t set, int tree) {
   if (tree == 0 && lds && set == kFtSets[0]) return (const void*)k_fused<true, kFtSets[0], 0>;
@@ -1041,6 +1031,10 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   // counter each): C2 grab sweep (profiles/r1_grab_sweep.jsonl) 64 -> 128:
   // -4 % at 1-2 ranks' shares; 256 for small chunks: -11 % on the 8-GPU share
   p.grab_min = (uint32_t)std::max(1, env_int("RT_GRAB_MIN", K <= 8u ? 256 : 128));
+  // partitioned chunk counters (rt_path.h grab_chunk): 64 partitions interleaved in
+  // granules of 256 chunks; progress slices use one counter (their ranges are contiguous)
+  p.parts_log2 = (uint32_t)std::min(6, std::max(0, env_int("RT_PARTS_LOG2", 6)));
+  p.gran_log2 = (uint32_t)std::min(20, std::max(0, env_int("RT_GRAN_LOG2", 8)));
   p.wave_times = nullptr;
   p.recs_lds = f_recs ? 1u : 0u;
   p.seed = o.seed;
@@ -1100,6 +1094,7 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   const int slices = (mode == RT_MODE_FUSED && n_chunks > 0)
                          ? std::max(1, std::min(o.progress_slices, 1024))
                          : 1;
+  if (slices > 1) p.parts_log2 = 0;
   while ((int)st->prog_events.size() < slices) {
     hipEvent_t e;
     HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1161,8 +1156,8 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     for (int sl = 0; sl < slices; ++sl) {
       if (slices > 1) {  // chunks [n*sl/S, n*(sl+1)/S): the counter starts at the range
         p.n_chunks = (uint32_t)((uint64_t)n_chunks * (sl + 1) / slices);
-        if (sl > 0)
-          HIP_OK(hipMemsetD32Async((hipDeviceptr_t)&st->ctr->chunk_head,
+        if (sl > 0)  // one partition (parts_log2 = 0 with slices): its counter is the head
+          HIP_OK(hipMemsetD32Async((hipDeviceptr_t)&st->ctr->part[0],
                                    (int)((uint64_t)n_chunks * sl / slices), 1, stream));
       }
       HIP_OK(hipLaunchKernel(fused_kernel, dim3(fused_blocks), dim3(256), args, fused_lds, stream));

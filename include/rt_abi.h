@@ -288,7 +288,8 @@ typedef struct {
 /* scene features (rt_scene_info.features, rt_stats.kernel_features) */
 enum {
   RT_FT_SPHERE = 1, RT_FT_TRI = 2, RT_FT_METAL = 4, RT_FT_DIEL = 8, RT_FT_MEDIA = 16,
-  RT_FT_CHECKER = 32, RT_FT_IMAGE = 64, RT_FT_NOISE = 128
+  RT_FT_CHECKER = 32, RT_FT_IMAGE = 64, RT_FT_NOISE = 128,
+  RT_FT_BOX = 256 /* box leaves (NewBox as one BVH leaf; scenes above 256 world prims) */
 };
 int rt_scene_info_get(const rt_scene* s, rt_scene_info* out);
 

@@ -63,7 +63,10 @@ RT_RNG_FN rt_u32x4 rt_philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint3
      C5 -0.4 %, C2 +-0, same words (profiles/r3_rng_unroll_ab.jsonl) */
 #pragma unroll
 #endif
-  for (int r = 0; r < 10; ++r) {
+#ifndef RT_PHILOX_ROUNDS
+#define RT_PHILOX_ROUNDS 10 /* other values: timing ablations only (not the parity stream) */
+#endif
+  for (int r = 0; r < RT_PHILOX_ROUNDS; ++r) {
     if (r) {
       k0 += RT_PHILOX_W0;
       k1 += RT_PHILOX_W1;

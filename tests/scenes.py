@@ -231,14 +231,38 @@ def obj_mixed(rt, asset_dir):
     return t, _cam(rt, (0, 3, -9), (0, 2.5, 0), spp=25), world, lights
 
 
+def box_leaves(rt, asset_dir):
+    """64 NewBoxes (384 quads: above the box-leaf threshold) with RotateY/Translate and
+    an image texture on some (alpha, beta of a box face), plus a metal sphere: the world
+    BVH holds box leaves (host_flatten.cpp; rt_kernels.h hit_box_rec)."""
+    with open(f"{asset_dir}/earthmap.ppm", "rb") as f:
+        data = f.read()
+    parts = data.split(b"\n", 3)
+    w, h = map(int, parts[1].split())
+    rgb = np.frombuffer(parts[3], np.uint8).reshape(h, w, 3)
+    t = rt.Tree(7)
+    world, lights = _room(t)
+    green = t.lambertian((0.48, 0.83, 0.53))
+    em = t.lambertian(t.image(rgb))
+    bl = t.list()
+    for i in range(8):
+        for j in range(8):
+            x0, z0 = -8 + 2 * i, -8 + 2 * j
+            b = t.box((0, 0, 0), (1.6, t.rand_range(0.3, 2.5), 1.2), em if (i + j) % 3 == 0 else green)
+            t.add(bl, t.translate(t.rotate_y(b, 37 * i + 11 * j), (x0 + 0.5, 0, z0 + 0.5)))
+    t.add(world, t.bvh(bl))
+    t.add(world, t.sphere((0, 3.5, 0), 1, t.metal((0.8, 0.8, 0.9), 0.1)))
+    return t, _cam(rt, (0, 7, -13), (0, 1, 0)), world, lights
+
+
 FEATURES = ["fog", "water", "earth", "cluster", "metal_fuzz", "glass", "boxes", "marble", "motion",
             "sphere_light", "tri_mesh", "nested_lights", "smoke_box", "dup_medium", "no_lights",
-            "checker", "obj_mixed"]
+            "checker", "obj_mixed", "box_leaves"]
 
 
 def build(rt, name, asset_dir):
     fn = globals()[name]
-    if name in ("earth", "obj_mixed"):
+    if name in ("earth", "obj_mixed", "box_leaves"):
         return fn(rt, asset_dir)
     return fn(rt)
 

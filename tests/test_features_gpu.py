@@ -51,8 +51,32 @@ def test_noise_tables_kernel_choice(rt, oracle, gpu, tables):
     with rt.Scene(t, world, lights) as sc:
         img, st = sc.render(cam, seed=5)
     ref, _ = oracle.render(t, world, lights, cam, seed=5, threads=8)
-    assert (st["kernel_features"] == 255) == (tables > 1), st["kernel_features"]
+    assert (st["kernel_features"] == rt.RT_FT_ALL) == (tables > 1), st["kernel_features"]
     m = compare(img, ref)
     # measured 0.9971 / 1.0 (profiles/r3_parity_v5.jsonl)
     assert m["frac_close"] >= 0.995, m
     assert m["q_equal"] >= 0.995, m
+
+
+def test_box_leaves_match_per_quad_faces(rt, oracle, gpu, monkeypatch):
+    """Box leaves (one slab test per NewBox, rt_kernels.h hit_box_rec) against the same
+    scene built with the six quads as leaves (RT_BOX_LEAVES=0): the two differ only
+    where the slab and the quad tests round differently at box edges, and both meet P1
+    against the oracle.  Includes image-textured faces (alpha, beta derived in
+    shade_core from the face's quad record) and rotated boxes."""
+    t, cam, w, l = scenes.build(rt, "box_leaves", ASSETS)
+    with rt.Scene(t, w, l) as sc:
+        assert sc.info()["features"] & rt.RT_FT_BOX
+        on, st_on = sc.render(cam, seed=4)
+    monkeypatch.setenv("RT_BOX_LEAVES", "0")
+    with rt.Scene(t, w, l) as sc:
+        assert not sc.info()["features"] & rt.RT_FT_BOX
+        off, st_off = sc.render(cam, seed=4)
+    ref, ost = oracle.render(t, w, l, cam, seed=4, threads=8)
+    m_on, m_off, m_pair = compare(on, ref), compare(off, ref), compare(on, off)
+    print(m_on, m_off, m_pair)
+    for m in (m_on, m_off):
+        assert m["frac_close"] >= p1_bar("box_leaves", "frac_close"), m
+        assert m["q_equal"] >= p1_bar("box_leaves", "q_equal"), m
+    assert m_pair["q_equal"] >= 0.995, m_pair
+    assert abs(st_on["segments"] - st_off["segments"]) <= 0.01 * st_off["segments"]

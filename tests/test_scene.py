@@ -22,7 +22,9 @@ def test_cornell_flattening(rt):
 
 def test_book2_flattening(rt):
     i = info(rt, "book2")
-    assert i["n_world_prims"] == 2400 + 1 + 1006  # boxes, light, spheres (1000 rotated)
+    # 400 ground boxes as box leaves (host_flatten.cpp), light, spheres (1000 rotated)
+    assert i["n_world_prims"] == 400 + 1 + 1006
+    assert i["features"] & rt.RT_FT_BOX
     assert i["n_media"] == 2 and i["medium_draws"] == 2  # flat world list: no duplication
     assert i["n_images"] == 1 and i["n_perlins"] == 1
 
@@ -213,3 +215,28 @@ def test_bvh_build_is_thread_count_invariant(rt, monkeypatch):
             nodes, refs, root, bounds = sc.export_bvh()
         out[th] = (nodes.tobytes(), refs.tobytes(), int(root), bounds.tobytes())
     assert out["1"] == out["3"] == out["8"]
+
+
+def test_box_leaves_kept_only_where_they_pay(rt, monkeypatch):
+    """NewBox becomes one BVH leaf (rt_device.h "box leaf") in large scenes whose kernel
+    set has FT_BOX; small scenes and lean sets keep the six quads, so their trees and
+    images are exactly the per-quad ones."""
+    import os
+    from tests import scenes
+    assets = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets")
+    t, cam, w, l = scenes.box_leaves(rt, assets)
+    with rt.Scene(t, w, l) as sc:
+        i = sc.info()
+        bvh_invariants(sc)
+    assert i["features"] & rt.RT_FT_BOX and i["n_world_prims"] == 64 + 3 + 1
+    monkeypatch.setenv("RT_BOX_LEAVES", "0")
+    with rt.Scene(t, w, l) as sc:
+        j = sc.info()
+    assert not j["features"] & rt.RT_FT_BOX and j["n_world_prims"] == 6 * 64 + 3 + 1
+    assert j["n_quads"] == i["n_quads"]  # the same quads either way
+    monkeypatch.delenv("RT_BOX_LEAVES")
+    for name in ("cornell", "quads"):  # small: no box leaves
+        assert not info(rt, name)["features"] & rt.RT_FT_BOX
+    t, cam, w, l = scenes.boxes(rt)  # 216 quads, lean set: expanded
+    with rt.Scene(t, w, l) as sc:
+        assert not sc.info()["features"] & rt.RT_FT_BOX

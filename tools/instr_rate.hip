@@ -1,0 +1,185 @@
+// Issue cost of the integer and fp ops the path tracer's RNG and traversal use (dev tool):
+// hipcc --offload-arch=gfx950 -O3 tools/instr_rate.hip -o /tmp/instr_rate && /tmp/instr_rate
+// Each kernel runs 8 independent chains of one instruction per lane for ITERS iterations;
+// the result is SIMD cycles per wave-instruction, at 1 wave per SIMD and at 8 waves per SIMD
+// (the device-wide throughput: elapsed clock x SIMDs / instructions issued).
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdint.h>
+
+#define ITERS 4096
+
+#define BODY8(OP) OP(0) OP(1) OP(2) OP(3) OP(4) OP(5) OP(6) OP(7)
+
+__global__ void k_mad_u64(uint32_t* out, uint32_t seed) {
+  uint64_t a[8];
+  uint32_t m = 0xD2511F53u ^ seed;
+  for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
+  for (int it = 0; it < ITERS; ++it) {
+#define OP(i) asm volatile("v_mad_u64_u32 %0, null, %1, %2, 0" : "=v"(a[i]) : "v"((uint32_t)a[i]), "s"(m));
+    BODY8(OP)
+#undef OP
+  }
+  uint32_t s = 0;
+  for (int i = 0; i < 8; ++i) s ^= (uint32_t)a[i] ^ (uint32_t)(a[i] >> 32);
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+__global__ void k_mul_hi(uint32_t* out, uint32_t seed) {
+  uint32_t a[8];
+  uint32_t m = 0xD2511F53u ^ seed;
+  for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
+  for (int it = 0; it < ITERS; ++it) {
+#define OP(i) asm volatile("v_mul_hi_u32 %0, %1, %2" : "=v"(a[i]) : "v"(a[i]), "s"(m));
+    BODY8(OP)
+#undef OP
+  }
+  uint32_t s = 0;
+  for (int i = 0; i < 8; ++i) s ^= a[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+__global__ void k_mul_lo(uint32_t* out, uint32_t seed) {
+  uint32_t a[8];
+  uint32_t m = 0xD2511F53u ^ seed;
+  for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
+  for (int it = 0; it < ITERS; ++it) {
+#define OP(i) asm volatile("v_mul_lo_u32 %0, %1, %2" : "=v"(a[i]) : "v"(a[i]), "s"(m));
+    BODY8(OP)
+#undef OP
+  }
+  uint32_t s = 0;
+  for (int i = 0; i < 8; ++i) s ^= a[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+__global__ void k_mul_u24(uint32_t* out, uint32_t seed) {
+  uint32_t a[8];
+  uint32_t m = 0x511F53u ^ seed;
+  for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
+  for (int it = 0; it < ITERS; ++it) {
+#define OP(i) asm volatile("v_mul_u32_u24 %0, %1, %2" : "=v"(a[i]) : "v"(a[i]), "s"(m));
+    BODY8(OP)
+#undef OP
+  }
+  uint32_t s = 0;
+  for (int i = 0; i < 8; ++i) s ^= a[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+__global__ void k_xor(uint32_t* out, uint32_t seed) {
+  uint32_t a[8];
+  uint32_t m = 0xD2511F53u ^ seed;
+  for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
+  for (int it = 0; it < ITERS; ++it) {
+#define OP(i) asm volatile("v_xor_b32 %0, %1, %2" : "=v"(a[i]) : "v"(a[i]), "s"(m));
+    BODY8(OP)
+#undef OP
+  }
+  uint32_t s = 0;
+  for (int i = 0; i < 8; ++i) s ^= a[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+__global__ void k_fma(uint32_t* out, uint32_t seed) {
+  float a[8];
+  float m = 1.0000001f + (float)seed;
+  for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
+  for (int it = 0; it < ITERS; ++it) {
+#define OP(i) asm volatile("v_fma_f32 %0, %1, %2, %1" : "=v"(a[i]) : "v"(a[i]), "s"(m));
+    BODY8(OP)
+#undef OP
+  }
+  float s = 0;
+  for (int i = 0; i < 8; ++i) s += a[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = __float_as_uint(s);
+}
+typedef float v2f __attribute__((ext_vector_type(2)));
+__global__ void k_pk_fma(uint32_t* out, uint32_t seed) {
+  v2f a[8];
+  v2f m = {1.0000001f + (float)seed, 1.0000002f};
+  for (int i = 0; i < 8; ++i) a[i] = v2f{(float)threadIdx.x, (float)i};
+  for (int it = 0; it < ITERS; ++it) {
+#define OP(i) asm volatile("v_pk_fma_f32 %0, %1, %2, %1" : "=v"(a[i]) : "v"(a[i]), "v"(m));
+    BODY8(OP)
+#undef OP
+  }
+  float s = 0;
+  for (int i = 0; i < 8; ++i) s += a[i].x + a[i].y;
+  out[blockIdx.x * blockDim.x + threadIdx.x] = __float_as_uint(s);
+}
+__global__ void k_fma64(uint32_t* out, uint32_t seed) {
+  double a[8];
+  double m = 1.0000001 + (double)seed;
+  for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
+  for (int it = 0; it < ITERS; ++it) {
+#define OP(i) asm volatile("v_fma_f64 %0, %1, %2, %1" : "=v"(a[i]) : "v"(a[i]), "v"(m));
+    BODY8(OP)
+#undef OP
+  }
+  double s = 0;
+  for (int i = 0; i < 8; ++i) s += a[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)s;
+}
+__global__ void k_rcp(uint32_t* out, uint32_t seed) {
+  float a[8];
+  for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i + 1 + seed;
+  for (int it = 0; it < ITERS; ++it) {
+#define OP(i) asm volatile("v_rcp_f32 %0, %1" : "=v"(a[i]) : "v"(a[i]));
+    BODY8(OP)
+#undef OP
+  }
+  float s = 0;
+  for (int i = 0; i < 8; ++i) s += a[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = __float_as_uint(s);
+}
+__global__ void k_cvt_f64(uint32_t* out, uint32_t seed) {
+  double a[8];
+  float f[8];
+  for (int i = 0; i < 8; ++i) f[i] = threadIdx.x * 7 + i + 1 + seed;
+  for (int it = 0; it < ITERS; ++it) {
+#define OP(i) asm volatile("v_cvt_f64_f32 %0, %1" : "=v"(a[i]) : "v"(f[i]));
+    BODY8(OP)
+#undef OP
+  }
+  double s = 0;
+  for (int i = 0; i < 8; ++i) s += a[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)s;
+}
+
+typedef void (*K)(uint32_t*, uint32_t);
+
+static void run(const char* name, K k, uint32_t* d) {
+  hipDeviceProp_t p;
+  hipGetDeviceProperties(&p, 0);
+  const int cus = p.multiProcessorCount;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  for (int waves_per_simd : {1, 2, 4, 8}) {
+    const int blocks = cus * waves_per_simd;  // 256-thread blocks: one wave per SIMD each
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, 0, d, 1u);
+    hipEventRecord(e0);
+    for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, 0, d, 1u);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    const double insts_per_simd = 5.0 * waves_per_simd * ITERS * 8;  // wave-instructions
+    const double cyc = ms * 1e-3 / 5.0 * 2.4e9;  // at 2.4 GHz nominal
+    printf("{\"instr\": \"%s\", \"waves_per_simd\": %d, \"cycles_per_wave_instr\": %.2f}\n", name,
+           waves_per_simd, cyc * 5.0 / insts_per_simd);
+  }
+}
+
+int main() {
+  uint32_t* d;
+  hipMalloc(&d, 256 * 2048 * sizeof(uint32_t));
+  run("v_mad_u64_u32", k_mad_u64, d);
+  run("v_mul_hi_u32", k_mul_hi, d);
+  run("v_mul_lo_u32", k_mul_lo, d);
+  run("v_mul_u32_u24", k_mul_u24, d);
+  run("v_xor_b32", k_xor, d);
+  run("v_fma_f32", k_fma, d);
+  run("v_pk_fma_f32", k_pk_fma, d);
+  run("v_fma_f64", k_fma64, d);
+  run("v_rcp_f32", k_rcp, d);
+  run("v_cvt_f64_f32", k_cvt_f64, d);
+  hipFree(d);
+  return 0;
+}
