@@ -401,12 +401,39 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
       // memory round trips per step; here it waits for one (C3 -1.7 %, C4 -4.9 %,
       // C5 -2.8 %, profiles/r3_unified_fetch_ab.jsonl).
       const bool leaf = (cur & LEAF_BIT) != 0u;
+      const bool trin = HAS(FT_TRI) && (cur & (LEAF_BIT | TRI_NODE_BIT)) == TRI_NODE_BIT;
       const uint32_t first = (cur >> 4) & 0x7FFFFFFu;
-      const F4* g = leaf ? sc.leafprims + 4 * (size_t)first : sc.nodes + 8 * (size_t)cur;
+      const F4* g = leaf   ? sc.leafprims + 4 * (size_t)first
+                    : trin ? sc.leafprims + (cur & (TRI_NODE_BIT - 1u))
+                           : sc.nodes + 8 * (size_t)cur;
       F4 v[7];
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = ld_glb(g + e);
-      if (!leaf) {
+      if (HAS(FT_TRI) && trin) {
+        // tri node (rt_device.h): its up to four triangles tested here, with the leaf
+        // test's arithmetic (hit_tri_rec, objects.go:408-461), instead of four boxes and a
+        // leaf step per box hit
+        F4 w[6];
+#pragma unroll
+        for (int e = 0; e < 6; ++e) w[e] = ld_glb(g + 4 + e);
+        const float f[40] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w,
+                             v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w,
+                             w[0].x, w[0].y, w[0].z, w[0].w, w[1].x, w[1].y, w[1].z, w[1].w,
+                             w[2].x, w[2].y, w[2].z, w[2].w, w[3].x, w[3].y, w[3].z, w[3].w,
+                             w[4].x, w[4].y, w[4].z, w[4].w, w[5].x, w[5].y, w[5].z, w[5].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float* q = f + 10 * k;
+          const F4 rec[3] = {{q[0], q[1], q[2], q[9]}, {q[3], q[4], q[5], 0.0f}, {q[6], q[7], q[8], 0.0f}};
+          float t, u, vv;
+          if (hit_tri_rec(rec, o, d, tmin, tr.best.t, t, u, vv)) {
+            tr.best.t = t;
+            tr.best.u = u;
+            tr.best.v = vv;
+            tr.best.ref = fbits(q[9]);
+          }
+        }
+      } else if (!leaf) {
 #pragma unroll
         for (int e = 4; e < 7; ++e) v[e] = ld_glb(g + e);
         const float tmax = tr.best.t;
@@ -1860,7 +1887,8 @@ RT_D uint32_t part_chunk(const Params& P, uint32_t p, uint32_t pos) {
   return ((((pos >> gl) << P.parts_log2) + p) << gl) | (pos & ((1u << gl) - 1u));
 }
 RT_D WaveBatch batch_init(const Params& P) {
-  const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  // wave-uniform (readfirstlane): the batch lives in SGPRs, not in VGPRs of every lane
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   return {0u, 0u, wave & ((1u << P.parts_log2) - 1u), 0ull};
 }
 RT_D uint32_t grab_chunk(const Params& P, WaveBatch& b, bool need) {

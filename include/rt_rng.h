@@ -75,8 +75,15 @@ RT_RNG_FN rt_u32x4 rt_philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint3
     uint64_t p1 = (uint64_t)RT_PHILOX_M1 * (uint64_t)c2;
     uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
     uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(RT_RNG_XOR2)
+    /* gfx950 v_bitop3_b32 (truth table 0x96 = a ^ b ^ c): one instruction per
+       three-way xor where hipcc emits two v_xor_b32; the same words */
+    uint32_t n0 = __builtin_amdgcn_bitop3_b32(hi1, c1, k0, 0x96);
+    uint32_t n2 = __builtin_amdgcn_bitop3_b32(hi0, c3, k1, 0x96);
+#else
     uint32_t n0 = hi1 ^ c1 ^ k0;
     uint32_t n2 = hi0 ^ c3 ^ k1;
+#endif
     c0 = n0;
     c1 = lo1;
     c2 = n2;

@@ -233,8 +233,9 @@ def obj_mixed(rt, asset_dir):
 
 def box_leaves(rt, asset_dir):
     """64 NewBoxes (384 quads: above the box-leaf threshold) with RotateY/Translate and
-    an image texture on some (alpha, beta of a box face), plus a metal sphere: the world
-    BVH holds box leaves (host_flatten.cpp; rt_kernels.h hit_box_rec)."""
+    an image texture on some (alpha, beta of a box face), plus a metal sphere and a
+    triangle (so the all-features kernel runs, the one with FT_BOX): the world BVH holds
+    box leaves (host_flatten.cpp; rt_kernels.h hit_box_rec)."""
     with open(f"{asset_dir}/earthmap.ppm", "rb") as f:
         data = f.read()
     parts = data.split(b"\n", 3)
@@ -252,6 +253,7 @@ def box_leaves(rt, asset_dir):
             t.add(bl, t.translate(t.rotate_y(b, 37 * i + 11 * j), (x0 + 0.5, 0, z0 + 0.5)))
     t.add(world, t.bvh(bl))
     t.add(world, t.sphere((0, 3.5, 0), 1, t.metal((0.8, 0.8, 0.9), 0.1)))
+    t.add(world, t.triangle([(-6, 0.5, 8), (6, 0.5, 8), (0, 5, 8.5)], t.lambertian((0.65, 0.05, 0.05))))
     return t, _cam(rt, (0, 7, -13), (0, 1, 0)), world, lights
 
 

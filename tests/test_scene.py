@@ -22,9 +22,9 @@ def test_cornell_flattening(rt):
 
 def test_book2_flattening(rt):
     i = info(rt, "book2")
-    # 400 ground boxes as box leaves (host_flatten.cpp), light, spheres (1000 rotated)
-    assert i["n_world_prims"] == 400 + 1 + 1006
-    assert i["features"] & rt.RT_FT_BOX
+    # ground boxes as 6 quads each: the book2 kernel set has no box leaves (rt_device.h)
+    assert i["n_world_prims"] == 2400 + 1 + 1006  # boxes, light, spheres (1000 rotated)
+    assert not i["features"] & rt.RT_FT_BOX
     assert i["n_media"] == 2 and i["medium_draws"] == 2  # flat world list: no duplication
     assert i["n_images"] == 1 and i["n_perlins"] == 1
 
@@ -228,11 +228,11 @@ def test_box_leaves_kept_only_where_they_pay(rt, monkeypatch):
     with rt.Scene(t, w, l) as sc:
         i = sc.info()
         bvh_invariants(sc)
-    assert i["features"] & rt.RT_FT_BOX and i["n_world_prims"] == 64 + 3 + 1
+    assert i["features"] & rt.RT_FT_BOX and i["n_world_prims"] == 64 + 3 + 1 + 1
     monkeypatch.setenv("RT_BOX_LEAVES", "0")
     with rt.Scene(t, w, l) as sc:
         j = sc.info()
-    assert not j["features"] & rt.RT_FT_BOX and j["n_world_prims"] == 6 * 64 + 3 + 1
+    assert not j["features"] & rt.RT_FT_BOX and j["n_world_prims"] == 6 * 64 + 3 + 1 + 1
     assert j["n_quads"] == i["n_quads"]  # the same quads either way
     monkeypatch.delenv("RT_BOX_LEAVES")
     for name in ("cornell", "quads"):  # small: no box leaves

@@ -4,6 +4,8 @@
 // the result is SIMD cycles per wave-instruction, at 1 wave per SIMD and at 8 waves per SIMD
 // (the device-wide throughput: elapsed clock x SIMDs / instructions issued).
 #include <hip/hip_runtime.h>
+#pragma clang diagnostic ignored "-Wunused-value"
+#pragma clang diagnostic ignored "-Wunused-result"
 #include <stdio.h>
 #include <stdint.h>
 
@@ -16,7 +18,7 @@ __global__ void k_mad_u64(uint32_t* out, uint32_t seed) {
   uint32_t m = 0xD2511F53u ^ seed;
   for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
   for (int it = 0; it < ITERS; ++it) {
-#define OP(i) asm volatile("v_mad_u64_u32 %0, null, %1, %2, 0" : "=v"(a[i]) : "v"((uint32_t)a[i]), "s"(m));
+#define OP(i) { uint64_t cc; asm volatile("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(a[i]), "=s"(cc) : "v"((uint32_t)a[i]), "s"(m)); }
     BODY8(OP)
 #undef OP
   }
