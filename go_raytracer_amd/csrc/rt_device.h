@@ -40,15 +40,8 @@ inline constexpr uint32_t leaf_code(uint32_t first, uint32_t count) {
 // ---- BVH4 node: four children's boxes in the parent, SoA (128 B) -----------
 //  f4[0] = lo.x of children 0..3   f4[1] = hi.x   f4[2] = lo.y   f4[3] = hi.y
 //  f4[4] = lo.z                   f4[5] = hi.z   f4[6] = child codes (bits)  f4[7] = 0
-// child code: inner BVH4 node index, leaf code (LEAF_BIT, as BVH2), tri node
-// (TRI_NODE_BIT | F4 offset into the leaf records), or CHILD_EMPTY
+// child code: inner BVH4 node index, leaf code (LEAF_BIT, as BVH2), or CHILD_EMPTY
 constexpr uint32_t CHILD_EMPTY = 0xFFFFFFFEu;
-// ---- tri node (large triangle scenes, rt_render.hip make_tri_nodes): a BVH4 node whose
-// children were all single-triangle leaves, replaced by the triangles themselves, so the
-// step that reaches it tests them directly instead of four boxes and then one leaf step
-// per box hit.  10 F4 (160 B) in the leaf-record array: triangle k at floats 10k..10k+9
-// = v0.xyz, e0.xyz, e1.xyz, ref bits; unused slots e0 = e1 = 0 (det = 0: never hit).
-constexpr uint32_t TRI_NODE_BIT = 0x40000000u;  // inner node indices stay below 2^30
 
 // ---- BVH8 node: eight children, 16-bit planes relative to the node's box (128 B)
 //  f4[0] = origin.xyz | biased exponents (bytes 0-2: plane = origin + q * 2^(E-127))

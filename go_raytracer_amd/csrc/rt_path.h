@@ -289,8 +289,9 @@ RT_D void camera_ray_r(const Params& P, const Ids& id, uint32_t sample, const rt
       c4 = {P.dku[0], P.dku[1], P.dku[2], 0.0f};
       c5 = {P.dkv[0], P.dkv[1], P.dkv[2], 0.0f};
     }
-    rt_u32x4 q = rt_rng_draw(P.seed, id.gpix, sample, RT_STREAM_CAMERA | 1u);
-    f3 dk = uniform_disk(rt_unit_f(q.v[0]), rt_unit_f(q.v[1]));
+    // the disk's two uniforms are the halves of camera word [3] (rt_rng.h): no second
+    // Philox call per defocused camera ray (C3, C5)
+    f3 dk = uniform_disk(rt_unit16_hi_f(r.v[3]), rt_unit16_lo_f(r.v[3]));
     f3 off = mk3(c4.x, c4.y, c4.z) * dk.x + mk3(c5.x, c5.y, c5.z) * dk.y;
     o = o + off;
     d = d - off;
@@ -401,39 +402,12 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
       // memory round trips per step; here it waits for one (C3 -1.7 %, C4 -4.9 %,
       // C5 -2.8 %, profiles/r3_unified_fetch_ab.jsonl).
       const bool leaf = (cur & LEAF_BIT) != 0u;
-      const bool trin = HAS(FT_TRI) && (cur & (LEAF_BIT | TRI_NODE_BIT)) == TRI_NODE_BIT;
       const uint32_t first = (cur >> 4) & 0x7FFFFFFu;
-      const F4* g = leaf   ? sc.leafprims + 4 * (size_t)first
-                    : trin ? sc.leafprims + (cur & (TRI_NODE_BIT - 1u))
-                           : sc.nodes + 8 * (size_t)cur;
+      const F4* g = leaf ? sc.leafprims + 4 * (size_t)first : sc.nodes + 8 * (size_t)cur;
       F4 v[7];
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = ld_glb(g + e);
-      if (HAS(FT_TRI) && trin) {
-        // tri node (rt_device.h): its up to four triangles tested here, with the leaf
-        // test's arithmetic (hit_tri_rec, objects.go:408-461), instead of four boxes and a
-        // leaf step per box hit
-        F4 w[6];
-#pragma unroll
-        for (int e = 0; e < 6; ++e) w[e] = ld_glb(g + 4 + e);
-        const float f[40] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w,
-                             v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w,
-                             w[0].x, w[0].y, w[0].z, w[0].w, w[1].x, w[1].y, w[1].z, w[1].w,
-                             w[2].x, w[2].y, w[2].z, w[2].w, w[3].x, w[3].y, w[3].z, w[3].w,
-                             w[4].x, w[4].y, w[4].z, w[4].w, w[5].x, w[5].y, w[5].z, w[5].w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float* q = f + 10 * k;
-          const F4 rec[3] = {{q[0], q[1], q[2], q[9]}, {q[3], q[4], q[5], 0.0f}, {q[6], q[7], q[8], 0.0f}};
-          float t, u, vv;
-          if (hit_tri_rec(rec, o, d, tmin, tr.best.t, t, u, vv)) {
-            tr.best.t = t;
-            tr.best.u = u;
-            tr.best.v = vv;
-            tr.best.ref = fbits(q[9]);
-          }
-        }
-      } else if (!leaf) {
+      if (!leaf) {
 #pragma unroll
         for (int e = 4; e < 7; ++e) v[e] = ld_glb(g + e);
         const float tmax = tr.best.t;
@@ -1897,13 +1871,13 @@ RT_D uint32_t grab_chunk(const Params& P, WaveBatch& b, bool need) {
   const uint32_t n = (uint32_t)__popcll(m);
   const uint32_t r = prefix_count(m);
   const uint32_t avail = b.end - b.next;
-  uint32_t pos, part;
+  // per lane only the chunk id: positions are mapped with the (uniform) partition of
+  // the batch they come from, so no per-lane partition or position stays live
+  uint32_t c = r < avail && b.part < (uint32_t)kMaxParts ? part_chunk(P, b.part, b.next + r)
+                                                         : 0xFFFFFFFFu;
   if (n <= avail) {
-    pos = b.next + r;
-    part = b.part;
     b.next = __builtin_amdgcn_readfirstlane(b.next + n);
   } else {
-    const uint32_t old_next = b.next, old_part = b.part;
     const uint32_t leader = (uint32_t)(__ffsll((long long)m) - 1);
     const uint32_t np = 1u << P.parts_log2;
     uint32_t g = 0u, gend = 0u;
@@ -1937,14 +1911,13 @@ RT_D uint32_t grab_chunk(const Params& P, WaveBatch& b, bool need) {
       b.part = __builtin_amdgcn_readfirstlane((sh + (uint32_t)(__ffsll((long long)rot) - 1)) & 63u);
     }
     const uint32_t take = r - avail;  // this lane's offset in the new batch (r >= avail)
-    pos = r < avail ? old_next + r : g + take;
-    part = r < avail ? old_part : b.part;
-    if (r >= avail && (b.part >= (uint32_t)kMaxParts || g + take >= gend)) part = (uint32_t)kMaxParts;
+    if (r >= avail)
+      c = b.part < (uint32_t)kMaxParts && g + take < gend ? part_chunk(P, b.part, g + take)
+                                                          : 0xFFFFFFFFu;
     b.next = __builtin_amdgcn_readfirstlane(min(g + (n - avail), gend));
     b.end = __builtin_amdgcn_readfirstlane(gend);
   }
-  if (!need || part >= (uint32_t)kMaxParts) return 0xFFFFFFFFu;
-  const uint32_t c = part_chunk(P, part, pos);
+  if (!need) return 0xFFFFFFFFu;
   return c < P.n_chunks ? c : 0xFFFFFFFFu;
 }
 

@@ -182,7 +182,6 @@ struct DeviceScene {
   const F4* brute_pairs = nullptr;  // quad records in pairs, largest first (record loop)
   size_t brute_slots = 0;           // records in brute_pairs, pads included (even)
   int32_t brute_boxes = 0;          // boxes among them tested as slabs (rt_path.h brute_box)
-  int32_t tri_nodes = 0;            // tri nodes in the BVH4 (make_tri_nodes)
   uint32_t root2 = PRIM_NONE;
   int32_t n_nodes2 = 0;
   ~DeviceScene() {
@@ -373,63 +372,6 @@ static void make_record(const HostScene& h, uint32_t ref, F4* r) {
   }
 }
 
-// Tri nodes (rt_device.h): in large scenes with triangles, every BVH4 node whose children
-// are all single-triangle leaves is referenced from its parent as a tri node instead: its
-// (up to four) triangles are appended to the leaf records as one 160-B tri node and the
-// parent's child code points there.  The closest hit is the same (every triangle the old
-// node could reach is tested; the interval test does the culling the boxes did).  The
-// host trees (export, BVH2) are unchanged.  Returns the number of tri nodes made.
-static size_t make_tri_nodes(const HostScene& h, std::vector<F4>& nodes4, std::vector<F4>& recs) {
-  const size_t nn = nodes4.size() / 8;
-  auto code_of = [&](size_t o, int k) {
-    uint32_t c;
-    memcpy(&c, &((const float*)&nodes4[8 * o + 6])[k], 4);
-    return c;
-  };
-  std::vector<int> all_tri(nn, 0);
-  for (size_t o = 0; o < nn; ++o) {
-    int n = 0;
-    bool ok = true;
-    for (int k = 0; k < 4 && ok; ++k) {
-      const uint32_t c = code_of(o, k);
-      if (c == CHILD_EMPTY) continue;
-      const uint32_t first = (c >> 4) & 0x7FFFFFFu;
-      ok = (c & LEAF_BIT) && (c & 15u) == 0u && (h.refs[first] >> 30) == PRIM_TRI;
-      ++n;
-    }
-    all_tri[o] = ok && n > 0;
-  }
-  size_t made = 0;
-  for (size_t o = 0; o < nn; ++o) {
-    float* cf = (float*)&nodes4[8 * o + 6];
-    for (int k = 0; k < 4; ++k) {
-      uint32_t c;
-      memcpy(&c, &cf[k], 4);
-      if ((c & LEAF_BIT) || c == CHILD_EMPTY || c >= nn || !all_tri[c]) continue;
-      const size_t off = recs.size();
-      if (off >= TRI_NODE_BIT) return made;  // offsets must fit below the flag bit
-      recs.resize(off + 10, F4{0, 0, 0, 0});
-      float* t = (float*)&recs[off];
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t cc = code_of(c, j);
-        uint32_t ref = PRIM_NONE;
-        if (cc != CHILD_EMPTY) {
-          ref = h.refs[(cc >> 4) & 0x7FFFFFFu];
-          const F4* tr = &h.tri[3 * (size_t)(ref & 0x3FFFFFFFu)];  // v0|mat, e0|area, e1|flags
-          const float f[9] = {tr[0].x, tr[0].y, tr[0].z, tr[1].x, tr[1].y, tr[1].z,
-                              tr[2].x, tr[2].y, tr[2].z};
-          memcpy(&t[10 * j], f, sizeof f);
-        }
-        memcpy(&t[10 * j + 9], &ref, 4);
-      }
-      const uint32_t code = TRI_NODE_BIT | (uint32_t)off;
-      memcpy(&cf[k], &code, 4);
-      ++made;
-    }
-  }
-  return made;
-}
-
 // the scene's device copy on `device` (uploaded on first use, then shared by every
 // slot on that device; read-only while rendering).  The scene-wide lock covers the
 // map lookup only; the upload holds its device's own lock, so first renders on
@@ -494,14 +436,7 @@ static int upload_scene(const Scene* s, DeviceScene* ds) {
   UP(h.quad, quad);
   UP(h.tri, tri);
   UP(h.tri_attr, tri_attr);
-  // tri nodes replace all-triangle bottom nodes in large trees (RT_TRI_NODES=0: off)
-  std::vector<F4> nodes4 = h.nodes4, recs;
-  build_leaf_records(h, recs);
-  const bool tri_nodes = env_int("RT_TRI_NODES", 1) != 0 && nodes4.size() / 8 >= 1024 &&
-                         std::any_of(h.refs.begin(), h.refs.end(),
-                                     [](uint32_t r) { return (r >> 30) == PRIM_TRI; });
-  ds->tri_nodes = tri_nodes ? (int32_t)make_tri_nodes(h, nodes4, recs) : 0;
-  UP(nodes4, nodes);
+  UP(h.nodes4, nodes);
   // the BVH2 and the record-loop pairs serve tiny scenes only (render_impl's tree
   // choice: <= 64 leaf entries); a 1M-triangle scene would upload 64 MB of BVH2
   const size_t tiny = (size_t)std::max(64, env_int("RT_BRUTE_MAX", kBruteMax));
@@ -511,7 +446,8 @@ static int upload_scene(const Scene* s, DeviceScene* ds) {
   ds->n_nodes2 = small ? (int32_t)(h.nodes.size() / 4) : 0;
   UP(h.refs, refs);
   {
-    std::vector<F4> lrecs;
+    std::vector<F4> recs, lrecs;
+    build_leaf_records(h, recs);
     UP(recs, leafprims);
     if (!h.refs8.empty()) {  // the BVH8's records, in its node order
       std::vector<F4> r8(4 * h.refs8.size());
@@ -1094,7 +1030,12 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   // chunks per refill of a wave's batch (one returning atomic on the chunk
   // counter each): C2 grab sweep (profiles/r1_grab_sweep.jsonl) 64 -> 128:
   // -4 % at 1-2 ranks' shares; 256 for small chunks: -11 % on the 8-GPU share
-  p.grab_min = (uint32_t)std::max(1, env_int("RT_GRAB_MIN", K <= 8u ? 256 : 128));
+  // Round 4, with the 64 partitioned counters below: batches of 32 chunks for the
+  // LDS-resident scenes (C2 -1.7 % on the whole image, its 8-GPU share 5.13 ms against
+  // 5.22 with 128; profiles/r4_share_probe_grab_v1.jsonl, r4_grab_ab.jsonl), while the
+  // scenes that traverse a tree through L1/L2 keep 128 (32 measured C3 +3.7 %, C4 +2.2 %,
+  // C5 +2 %: their waves refill more often and spread over more of the image)
+  p.grab_min = (uint32_t)std::max(1, env_int("RT_GRAB_MIN", f_lds ? 32 : K <= 8u ? 256 : 128));
   // partitioned chunk counters (rt_path.h grab_chunk): 64 partitions interleaved in
   // granules of 256 chunks; progress slices use one counter (their ranges are contiguous)
   p.parts_log2 = (uint32_t)std::min(6, std::max(0, env_int("RT_PARTS_LOG2", 6)));

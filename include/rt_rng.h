@@ -17,8 +17,11 @@
  *
  * Dimension map (one Philox call = 4 lanes):
  *   camera  group 0: [0] jitter x (inner stratum s_j)  [1] jitter y (outer s_i)
- *                    [2] ray time                       [3] unused
- *   camera  group 1: [0],[1] defocus disk (only when DefocusAngle > 0)
+ *                    [2] ray time
+ *                    [3] defocus disk (only when DefocusAngle > 0): its high and low
+ *                        16 bits as two 16-bit uniforms (rt_unit16_hi / _lo), so a
+ *                        defocused camera ray needs no second Philox call (round 4;
+ *                        round 3 drew them from a camera group-1 call)
  *   vertex k group 0: [0] coin (mixture pdf pdf.go:70 / dielectric materials.go:112)
  *                     [1] light pick (hittable.go:102 rand.Intn) — 24-bit integer
  *                     [2],[3] direction sample (cosine, light, sphere, fuzz)
@@ -121,6 +124,13 @@ RT_RNG_FN uint32_t rt_spare24(rt_u32x4 r) {
 RT_RNG_FN float rt_unit_f(uint32_t x) { return (float)(x >> 8) * 5.9604644775390625e-08f; }
 
 RT_RNG_FN double rt_unit_d(uint32_t x) { return (double)(x >> 8) * 5.9604644775390625e-08; }
+
+/* 16-bit uniforms from the two halves of a word (the defocus disk, camera word [3]):
+   exact in float and double, in [0, 1 - 2^-16] */
+RT_RNG_FN float rt_unit16_hi_f(uint32_t x) { return (float)(x >> 16) * 1.52587890625e-05f; }
+RT_RNG_FN float rt_unit16_lo_f(uint32_t x) { return (float)(x & 0xFFFFu) * 1.52587890625e-05f; }
+RT_RNG_FN double rt_unit16_hi_d(uint32_t x) { return (double)(x >> 16) * 1.52587890625e-05; }
+RT_RNG_FN double rt_unit16_lo_d(uint32_t x) { return (double)(x & 0xFFFFu) * 1.52587890625e-05; }
 
 /* rand.Intn(n) replacement: exact integer map of the 24-bit uniform to [0, n). */
 RT_RNG_FN uint32_t rt_pick(uint32_t x, uint32_t n) {

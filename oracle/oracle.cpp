@@ -973,8 +973,10 @@ struct Renderer {
     Vec3<R> ps = p00.add(du.scale((R)i + px)).add(dv.scale((R)j + py));
     Vec3<R> origin = center;
     if (cd.defocus > 0) {  // defocusDiskSample :285-290 (RandomUnitDisk, closed form)
-      rt_u32x4 q = c.draw(RT_STREAM_CAMERA | 1u);
-      R rr = std::sqrt(U<R>(q.v[0])), phi = R(2) * R(M_PI) * U<R>(q.v[1]);
+      // the disk's two uniforms: the halves of camera word [3] (rt_rng.h)
+      const R u0 = sizeof(R) == 4 ? (R)rt_unit16_hi_f(r.v[3]) : (R)rt_unit16_hi_d(r.v[3]);
+      const R u1 = sizeof(R) == 4 ? (R)rt_unit16_lo_f(r.v[3]) : (R)rt_unit16_lo_d(r.v[3]);
+      R rr = std::sqrt(u0), phi = R(2) * R(M_PI) * u1;
       Vec3<R> p(rr * std::cos(phi), rr * std::sin(phi), 0);
       origin = center.add(dku.scale(p.x())).add(dkv.scale(p.y()));
     }

@@ -144,6 +144,95 @@ __global__ void k_cvt_f64(uint32_t* out, uint32_t seed) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)s;
 }
 
+// generic: 8 independent chains of one VOP2/VOP3 op "OP dst, dst, s"
+#define K_BIN(NAME, ASM, T)                                                              \
+  __global__ void NAME(uint32_t* out, uint32_t seed) {                                    \
+    T a[8];                                                                              \
+    T m = (T)(1.0000001f + (float)seed);                                                 \
+    for (int i = 0; i < 8; ++i) a[i] = (T)(threadIdx.x * 7 + i);                         \
+    for (int it = 0; it < ITERS; ++it) {                                                 \
+      OPS_##NAME                                                                         \
+    }                                                                                    \
+    T s = 0;                                                                             \
+    for (int i = 0; i < 8; ++i) s += a[i];                                               \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)s;                            \
+  }
+#define CH(ASM, i) asm volatile(ASM : "+v"(a[i]) : "v"(m));
+#define CH8(ASM) CH(ASM, 0) CH(ASM, 1) CH(ASM, 2) CH(ASM, 3) CH(ASM, 4) CH(ASM, 5) CH(ASM, 6) CH(ASM, 7)
+#define OPS_k_add_f32 CH8("v_add_f32 %0, %0, %1")
+#define OPS_k_mul_f32 CH8("v_mul_f32 %0, %0, %1")
+#define OPS_k_max_f32 CH8("v_max_f32 %0, %0, %1")
+#define OPS_k_min3_f32 CH8("v_min3_f32 %0, %0, %1, %0")
+#define OPS_k_add_u32 CH8("v_add_u32 %0, %0, %1")
+#define OPS_k_and_b32 CH8("v_and_b32 %0, %0, %1")
+#define OPS_k_lshr_b32 CH8("v_lshrrev_b32 %0, 3, %0")
+#define OPS_k_mov_b32 CH8("v_mov_b32 %0, %1")
+#define OPS_k_cndmask CH8("v_cndmask_b32 %0, %0, %1, vcc")
+#define OPS_k_bitop3 CH8("v_bitop3_b32 %0, %0, %1, %0 bitop3:0x96")
+#define OPS_k_cvt_f32_u32 CH8("v_cvt_f32_u32 %0, %0")
+#define OPS_k_sqrt_f32 CH8("v_sqrt_f32 %0, %0")
+#define OPS_k_cmp_f32 CH8("v_cmp_lt_f32 vcc, %0, %1")
+K_BIN(k_add_f32, 0, float)
+K_BIN(k_mul_f32, 0, float)
+K_BIN(k_max_f32, 0, float)
+K_BIN(k_min3_f32, 0, float)
+K_BIN(k_add_u32, 0, uint32_t)
+K_BIN(k_and_b32, 0, uint32_t)
+K_BIN(k_lshr_b32, 0, uint32_t)
+K_BIN(k_mov_b32, 0, uint32_t)
+K_BIN(k_cndmask, 0, uint32_t)
+K_BIN(k_bitop3, 0, uint32_t)
+K_BIN(k_cvt_f32_u32, 0, uint32_t)
+K_BIN(k_sqrt_f32, 0, float)
+K_BIN(k_cmp_f32, 0, float)
+
+// selects: the mask set by a compare before the loop (vcc, or an SGPR pair through VOP3)
+__global__ void k_cndmask_vcc(uint32_t* out, uint32_t seed) {
+  uint32_t a[8];
+  uint32_t m = 0x12345u ^ seed;
+  for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
+  asm volatile("v_cmp_gt_u32 vcc, 32, %0" ::"v"(threadIdx.x) : "vcc");
+  for (int it = 0; it < ITERS; ++it) {
+#define OP(i) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a[i]) : "v"(m) : "vcc");
+    BODY8(OP)
+#undef OP
+  }
+  uint32_t s = 0;
+  for (int i = 0; i < 8; ++i) s ^= a[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+__global__ void k_cndmask_sgpr(uint32_t* out, uint32_t seed) {
+  uint32_t a[8];
+  uint32_t m = 0x12345u ^ seed;
+  for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
+  unsigned long long msk;
+  asm volatile("v_cmp_gt_u32 %0, 32, %1" : "=s"(msk) : "v"(threadIdx.x));
+  for (int it = 0; it < ITERS; ++it) {
+#define OP(i) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a[i]) : "v"(m), "s"(msk));
+    BODY8(OP)
+#undef OP
+  }
+  uint32_t s = 0;
+  for (int i = 0; i < 8; ++i) s ^= a[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+// compiler-generated selects: x = c ? y : x with c from a float compare each iteration
+__global__ void k_select_cc(uint32_t* out, uint32_t seed) {
+  float a[8], b[8];
+  for (int i = 0; i < 8; ++i) { a[i] = threadIdx.x * 7 + i; b[i] = (float)(seed + i); }
+  for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float t = b[i] * 1.0001f;
+      a[i] = t < a[i] ? t : a[i];
+      b[i] = t;
+    }
+  }
+  float s = 0;
+  for (int i = 0; i < 8; ++i) s += a[i] + b[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = __float_as_uint(s);
+}
+
 typedef void (*K)(uint32_t*, uint32_t);
 
 static void run(const char* name, K k, uint32_t* d) {
@@ -182,6 +271,22 @@ int main() {
   run("v_fma_f64", k_fma64, d);
   run("v_rcp_f32", k_rcp, d);
   run("v_cvt_f64_f32", k_cvt_f64, d);
+  run("v_add_f32", k_add_f32, d);
+  run("v_mul_f32", k_mul_f32, d);
+  run("v_max_f32", k_max_f32, d);
+  run("v_min3_f32", k_min3_f32, d);
+  run("v_add_u32", k_add_u32, d);
+  run("v_and_b32", k_and_b32, d);
+  run("v_lshrrev_b32", k_lshr_b32, d);
+  run("v_mov_b32", k_mov_b32, d);
+  run("v_cndmask_b32", k_cndmask, d);
+  run("v_bitop3_b32", k_bitop3, d);
+  run("v_cvt_f32_u32", k_cvt_f32_u32, d);
+  run("v_sqrt_f32", k_sqrt_f32, d);
+  run("v_cmp_lt_f32", k_cmp_f32, d);
+  run("v_cndmask_b32 (vcc set once)", k_cndmask_vcc, d);
+  run("v_cndmask_b32_e64 (sgpr mask)", k_cndmask_sgpr, d);
+  run("compiled select: mul + cmp + cndmask per element", k_select_cc, d);
   hipFree(d);
   return 0;
 }
