@@ -401,29 +401,45 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
       // whose lanes are split between nodes and leaves waited for two dependent
       // memory round trips per step; here it waits for one (C3 -1.7 %, C4 -4.9 %,
       // C5 -2.8 %, profiles/r3_unified_fetch_ab.jsonl).
+      // Node and leaf record share one allocation (rt_render.hip upload_scene): both are
+      // addressed as 32-bit byte offsets from the node base (global_load with an SGPR
+      // base).  A node's planes are fetched already ordered by the ray's direction signs:
+      // the near x plane of the four children is lo.x (offset 0) when inv.x >= 0 and hi.x
+      // (offset 16) when inv.x < 0, the far plane the other one, and likewise for y / z.
+      // The slab test then needs no min/max per axis (v_min/v_max_f32 issue at half the
+      // rate of v_sub/v_mul on gfx950, profiles/r4_instr_rate.jsonl): 16 min/max per node
+      // instead of 40.  The same planes as min/max would pick, so the same t0, t1.
       const bool leaf = (cur & LEAF_BIT) != 0u;
       const uint32_t first = (cur >> 4) & 0x7FFFFFFu;
-      const F4* g = leaf ? sc.leafprims + 4 * (size_t)first : sc.nodes + 8 * (size_t)cur;
+      const uint32_t rec0 = (uint32_t)((const char*)sc.leafprims - (const char*)sc.nodes);
+      const uint32_t off = leaf ? rec0 + (first << 6) : cur << 7;
+      const uint32_t nmask = leaf ? 0u : 16u;
+      const uint32_t sx = (fbits(inv.x) >> 27) & nmask, sy = (fbits(inv.y) >> 27) & nmask;
+      const char* nb = (const char*)sc.nodes;
       F4 v[7];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = ld_glb(g + e);
+      v[0] = ld_glb((const F4*)(nb + (off + sx)));
+      v[1] = ld_glb((const F4*)(nb + (off + (16u - sx))));
+      v[2] = ld_glb((const F4*)(nb + (off + (32u + sy))));
+      v[3] = ld_glb((const F4*)(nb + (off + (48u - sy))));
       if (!leaf) {
-#pragma unroll
-        for (int e = 4; e < 7; ++e) v[e] = ld_glb(g + e);
+        const uint32_t sz = (fbits(inv.z) >> 27) & 16u;
+        v[4] = ld_glb((const F4*)(nb + (off + (64u + sz))));
+        v[5] = ld_glb((const F4*)(nb + (off + (80u - sz))));
+        v[6] = ld_glb((const F4*)(nb + (off + 96u)));
         const float tmax = tr.best.t;
         float tn[4];
         uint32_t ch[4];
-        const float Lx[4] = {v[0].x, v[0].y, v[0].z, v[0].w}, Hx[4] = {v[1].x, v[1].y, v[1].z, v[1].w};
-        const float Ly[4] = {v[2].x, v[2].y, v[2].z, v[2].w}, Hy[4] = {v[3].x, v[3].y, v[3].z, v[3].w};
-        const float Lz[4] = {v[4].x, v[4].y, v[4].z, v[4].w}, Hz[4] = {v[5].x, v[5].y, v[5].z, v[5].w};
+        const float Nx[4] = {v[0].x, v[0].y, v[0].z, v[0].w}, Fx[4] = {v[1].x, v[1].y, v[1].z, v[1].w};
+        const float Ny[4] = {v[2].x, v[2].y, v[2].z, v[2].w}, Fy[4] = {v[3].x, v[3].y, v[3].z, v[3].w};
+        const float Nz[4] = {v[4].x, v[4].y, v[4].z, v[4].w}, Fz[4] = {v[5].x, v[5].y, v[5].z, v[5].w};
         const uint32_t C[4] = {fbits(v[6].x), fbits(v[6].y), fbits(v[6].z), fbits(v[6].w)};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const float tx0 = (Lx[k] - o.x) * inv.x, tx1 = (Hx[k] - o.x) * inv.x;
-          const float ty0 = (Ly[k] - o.y) * inv.y, ty1 = (Hy[k] - o.y) * inv.y;
-          const float tz0 = (Lz[k] - o.z) * inv.z, tz1 = (Hz[k] - o.z) * inv.z;
-          const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin));
-          const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax));
+          const float tx0 = (Nx[k] - o.x) * inv.x, tx1 = (Fx[k] - o.x) * inv.x;
+          const float ty0 = (Ny[k] - o.y) * inv.y, ty1 = (Fy[k] - o.y) * inv.y;
+          const float tz0 = (Nz[k] - o.z) * inv.z, tz1 = (Fz[k] - o.z) * inv.z;
+          const float t0 = fmaxf(fmaxf(tx0, ty0), fmaxf(tz0, tmin));
+          const float t1 = fminf(fminf(tx1, ty1), fminf(tz1, tmax));
           const bool h = t0 <= t1 * 1.00000024f && C[k] != CHILD_EMPTY;  // slab() semantics
           tn[k] = h ? t0 : kInf;
           ch[k] = C[k];

@@ -436,7 +436,22 @@ static int upload_scene(const Scene* s, DeviceScene* ds) {
   UP(h.quad, quad);
   UP(h.tri, tri);
   UP(h.tri_attr, tri_attr);
-  UP(h.nodes4, nodes);
+  // the BVH4 nodes and the leaf records in ONE allocation (nodes first): the traversal
+  // addresses both as 32-bit byte offsets from the node base (rt_path.h trav_steps)
+  std::vector<F4> recs;
+  build_leaf_records(h, recs);
+  {
+    std::vector<F4> tree_buf(h.nodes4);
+    tree_buf.resize((tree_buf.size() + 15) / 16 * 16, F4{0, 0, 0, 0});  // records 256-B aligned
+    const size_t rec0 = tree_buf.size();
+    if ((rec0 + recs.size()) * sizeof(F4) >= ((size_t)1 << 32))
+      return set_error(RT_ERR_UNSUPPORTED, "scene: BVH nodes + leaf records exceed 4 GiB");
+    tree_buf.insert(tree_buf.end(), recs.begin(), recs.end());
+    const F4* base = nullptr;
+    if ((rc = upload(ds, tree_buf, &base)) != RT_OK) return rc;
+    d.nodes = base;
+    d.leafprims = base ? base + rec0 : nullptr;
+  }
   // the BVH2 and the record-loop pairs serve tiny scenes only (render_impl's tree
   // choice: <= 64 leaf entries); a 1M-triangle scene would upload 64 MB of BVH2
   const size_t tiny = (size_t)std::max(64, env_int("RT_BRUTE_MAX", kBruteMax));
@@ -446,9 +461,7 @@ static int upload_scene(const Scene* s, DeviceScene* ds) {
   ds->n_nodes2 = small ? (int32_t)(h.nodes.size() / 4) : 0;
   UP(h.refs, refs);
   {
-    std::vector<F4> recs, lrecs;
-    build_leaf_records(h, recs);
-    UP(recs, leafprims);
+    std::vector<F4> lrecs;
     if (!h.refs8.empty()) {  // the BVH8's records, in its node order
       std::vector<F4> r8(4 * h.refs8.size());
       for (size_t i = 0; i < h.refs8.size(); ++i) make_record(h, h.refs8[i], &r8[4 * i]);

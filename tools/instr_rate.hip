@@ -233,6 +233,34 @@ __global__ void k_select_cc(uint32_t* out, uint32_t seed) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = __float_as_uint(s);
 }
 
+#define CHS(ASM, i) asm volatile(ASM : "+v"(a[i]) : "s"(m));
+#define CHS8(ASM) CHS(ASM, 0) CHS(ASM, 1) CHS(ASM, 2) CHS(ASM, 3) CHS(ASM, 4) CHS(ASM, 5) CHS(ASM, 6) CHS(ASM, 7)
+#define K_BINS(NAME, ASM, T)                                                             \
+  __global__ void NAME(uint32_t* out, uint32_t seed) {                                    \
+    T a[8];                                                                              \
+    T m = (T)(1.0000001f + (float)seed);                                                 \
+    for (int i = 0; i < 8; ++i) a[i] = (T)(threadIdx.x * 7 + i);                         \
+    for (int it = 0; it < ITERS; ++it) { CHS8(ASM) }                                     \
+    T s = 0;                                                                             \
+    for (int i = 0; i < 8; ++i) s += a[i];                                               \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)s;                            \
+  }
+K_BINS(k_xor_vs, "v_xor_b32_e64 %0, %0, %1", uint32_t)
+#define OPS_k_xor_vv CH8("v_xor_b32 %0, %0, %1")
+K_BIN(k_xor_vv, 0, uint32_t)
+K_BINS(k_max_vs, "v_max_f32_e64 %0, %0, %1", float)
+K_BINS(k_add_vs, "v_add_f32_e64 %0, %0, %1", float)
+K_BINS(k_and_vs, "v_and_b32_e64 %0, %0, %1", uint32_t)
+#define OPS_k_sub_f32 CH8("v_sub_f32 %0, %0, %1")
+K_BIN(k_sub_f32, 0, float)
+#define OPS_k_max3_f32 CH8("v_max3_f32 %0, %0, %1, %0")
+K_BIN(k_max3_f32, 0, float)
+#define OPS_k_max_u32 CH8("v_max_u32 %0, %0, %1")
+K_BIN(k_max_u32, 0, uint32_t)
+#define OPS_k_or_b32 CH8("v_or_b32 %0, %0, %1")
+K_BIN(k_or_b32, 0, uint32_t)
+#define OPS_k_lshl_add_u64 CH8("v_lshl_add_u64 %0, %0, 2, %1")
+
 typedef void (*K)(uint32_t*, uint32_t);
 
 static void run(const char* name, K k, uint32_t* d) {
@@ -287,6 +315,15 @@ int main() {
   run("v_cndmask_b32 (vcc set once)", k_cndmask_vcc, d);
   run("v_cndmask_b32_e64 (sgpr mask)", k_cndmask_sgpr, d);
   run("compiled select: mul + cmp + cndmask per element", k_select_cc, d);
+  run("v_xor_b32_e64 (sgpr operand)", k_xor_vs, d);
+  run("v_xor_b32 (vgpr operands)", k_xor_vv, d);
+  run("v_max_f32_e64 (sgpr operand)", k_max_vs, d);
+  run("v_add_f32_e64 (sgpr operand)", k_add_vs, d);
+  run("v_and_b32_e64 (sgpr operand)", k_and_vs, d);
+  run("v_sub_f32", k_sub_f32, d);
+  run("v_max3_f32", k_max3_f32, d);
+  run("v_max_u32", k_max_u32, d);
+  run("v_or_b32", k_or_b32, d);
   hipFree(d);
   return 0;
 }
