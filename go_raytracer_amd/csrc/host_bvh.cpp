@@ -442,8 +442,11 @@ int build_bvh(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi
     float* lx = &nd[0].x;  // the 8 F4 as 32 floats: [field][child]
     for (int k = 0; k < 4; ++k) {
       uint32_t code = CHILD_EMPTY;
-      Box b;  // empty slot: a point box at the origin, skipped by its code
-      for (int a = 0; a < 3; ++a) b.mn[a] = b.mx[a] = 0.0f;
+      // empty slot: an inverted infinite box (lo = +inf, hi = -inf), which the
+      // sign-selected slab test (rt_path.h trav_steps) never hits; the min/max slab
+      // tests (LDS trees) skip it by its code
+      Box b;
+      for (int a = 0; a < 3; ++a) b.mn[a] = INFINITY, b.mx[a] = -INFINITY;
       if (k < nkids[o]) {
         const TmpNode& c = tn[kids[o][k]];
         b = c.box;

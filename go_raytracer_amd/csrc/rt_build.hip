@@ -415,7 +415,9 @@ static int finalize_tree(HostScene& s, const std::vector<F4>& nlo, const std::ve
     for (int k = 0; k < 4; ++k) {
       const int c = kids[o][k];
       uint32_t code = CHILD_EMPTY;
-      float b[6] = {0, 0, 0, 0, 0, 0};
+      // an empty slot's box is inverted and infinite (lo = +inf, hi = -inf): the
+      // sign-selected slab test (rt_path.h trav_steps) never hits it
+      float b[6] = {INFINITY, -INFINITY, INFINITY, -INFINITY, INFINITY, -INFINITY};
       if (c >= 0) {
         code = code_of(c, idx4);
         const float t[6] = {nlo[c].x, nhi[c].x, nlo[c].y, nhi[c].y, nlo[c].z, nhi[c].z};

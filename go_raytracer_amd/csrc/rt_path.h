@@ -440,7 +440,8 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
           const float tz0 = (Nz[k] - o.z) * inv.z, tz1 = (Fz[k] - o.z) * inv.z;
           const float t0 = fmaxf(fmaxf(tx0, ty0), fmaxf(tz0, tmin));
           const float t1 = fminf(fminf(tx1, ty1), fminf(tz1, tmax));
-          const bool h = t0 <= t1 * 1.00000024f && C[k] != CHILD_EMPTY;  // slab() semantics
+          // (an empty slot's inverted infinite box gives t1 = -inf: no code check)
+          const bool h = t0 <= t1 * 1.00000024f;  // slab() semantics
           tn[k] = h ? t0 : kInf;
           ch[k] = C[k];
         }
