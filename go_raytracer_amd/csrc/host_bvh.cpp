@@ -452,11 +452,11 @@ int build_bvh(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi
         b = c.box;
         code = c.left >= 0 ? (uint32_t)out4[kids[o][k]] : leaf_of(c);
       }
-      for (int a = 0; a < 3; ++a) {
-        lx[(2 * a) * 4 + k] = b.mn[a];
-        lx[(2 * a + 1) * 4 + k] = b.mx[a];
+      for (int a = 0; a < 3; ++a) {  // rt_device.h "BVH4 node": codes, then the planes
+        lx[(1 + 2 * a) * 4 + k] = b.mn[a];
+        lx[(2 + 2 * a) * 4 + k] = b.mx[a];
       }
-      lx[6 * 4 + k] = bits(code);
+      lx[k] = bits(code);
     }
   }
   s.root4 = 0;

@@ -423,8 +423,8 @@ static int finalize_tree(HostScene& s, const std::vector<F4>& nlo, const std::ve
         const float t[6] = {nlo[c].x, nhi[c].x, nlo[c].y, nhi[c].y, nlo[c].z, nhi[c].z};
         memcpy(b, t, sizeof t);
       }
-      for (int f = 0; f < 6; ++f) lx[f * 4 + k] = b[f];
-      lx[6 * 4 + k] = bits(code);
+      for (int f = 0; f < 6; ++f) lx[(1 + f) * 4 + k] = b[f];  // rt_device.h "BVH4 node"
+      lx[k] = bits(code);
     }
   }
   s.root4 = 0;

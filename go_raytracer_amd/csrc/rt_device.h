@@ -38,8 +38,10 @@ inline constexpr uint32_t leaf_code(uint32_t first, uint32_t count) {
 }
 
 // ---- BVH4 node: four children's boxes in the parent, SoA (128 B) -----------
-//  f4[0] = lo.x of children 0..3   f4[1] = hi.x   f4[2] = lo.y   f4[3] = hi.y
-//  f4[4] = lo.z                   f4[5] = hi.z   f4[6] = child codes (bits)  f4[7] = 0
+//  f4[0] = child codes (bits) of children 0..3   f4[1] = lo.x   f4[2] = hi.x
+//  f4[3] = lo.y   f4[4] = hi.y   f4[5] = lo.z   f4[6] = hi.z   f4[7] = 0
+//  (codes first: they are fetched with the leaf-record-sized part of a traversal step's
+//  loads, so they arrive with the first planes, rt_path.h trav_steps)
 // child code: inner BVH4 node index, leaf code (LEAF_BIT, as BVH2), or CHILD_EMPTY
 constexpr uint32_t CHILD_EMPTY = 0xFFFFFFFEu;
 

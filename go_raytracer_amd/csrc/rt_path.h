@@ -415,24 +415,25 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
       const uint32_t off = leaf ? rec0 + (first << 6) : cur << 7;
       const uint32_t nmask = leaf ? 0u : 16u;
       const uint32_t sx = (fbits(inv.x) >> 27) & nmask, sy = (fbits(inv.y) >> 27) & nmask;
+      // (node: v[0] = the child codes, then near x, far x, near y; a leaf: its record)
       const char* nb = (const char*)sc.nodes;
       F4 v[7];
-      v[0] = ld_glb((const F4*)(nb + (off + sx)));
-      v[1] = ld_glb((const F4*)(nb + (off + (16u - sx))));
-      v[2] = ld_glb((const F4*)(nb + (off + (32u + sy))));
-      v[3] = ld_glb((const F4*)(nb + (off + (48u - sy))));
+      v[0] = ld_glb((const F4*)(nb + off));
+      v[1] = ld_glb((const F4*)(nb + (off + (16u + sx))));
+      v[2] = ld_glb((const F4*)(nb + (off + (32u - sx))));
+      v[3] = ld_glb((const F4*)(nb + (off + (48u + sy))));
       if (!leaf) {
         const uint32_t sz = (fbits(inv.z) >> 27) & 16u;
-        v[4] = ld_glb((const F4*)(nb + (off + (64u + sz))));
-        v[5] = ld_glb((const F4*)(nb + (off + (80u - sz))));
-        v[6] = ld_glb((const F4*)(nb + (off + 96u)));
+        v[4] = ld_glb((const F4*)(nb + (off + (64u - sy))));
+        v[5] = ld_glb((const F4*)(nb + (off + (80u + sz))));
+        v[6] = ld_glb((const F4*)(nb + (off + (96u - sz))));
         const float tmax = tr.best.t;
         float tn[4];
         uint32_t ch[4];
-        const float Nx[4] = {v[0].x, v[0].y, v[0].z, v[0].w}, Fx[4] = {v[1].x, v[1].y, v[1].z, v[1].w};
-        const float Ny[4] = {v[2].x, v[2].y, v[2].z, v[2].w}, Fy[4] = {v[3].x, v[3].y, v[3].z, v[3].w};
-        const float Nz[4] = {v[4].x, v[4].y, v[4].z, v[4].w}, Fz[4] = {v[5].x, v[5].y, v[5].z, v[5].w};
-        const uint32_t C[4] = {fbits(v[6].x), fbits(v[6].y), fbits(v[6].z), fbits(v[6].w)};
+        const float Nx[4] = {v[1].x, v[1].y, v[1].z, v[1].w}, Fx[4] = {v[2].x, v[2].y, v[2].z, v[2].w};
+        const float Ny[4] = {v[3].x, v[3].y, v[3].z, v[3].w}, Fy[4] = {v[4].x, v[4].y, v[4].z, v[4].w};
+        const float Nz[4] = {v[5].x, v[5].y, v[5].z, v[5].w}, Fz[4] = {v[6].x, v[6].y, v[6].z, v[6].w};
+        const uint32_t C[4] = {fbits(v[0].x), fbits(v[0].y), fbits(v[0].z), fbits(v[0].w)};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const float tx0 = (Nx[k] - o.x) * inv.x, tx1 = (Fx[k] - o.x) * inv.x;
@@ -529,7 +530,7 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
       // BVH4 node: four slab tests, children ordered front to back; the
       // nearest is visited next, the others pushed farthest first
       const F4* g = LDS ? lnodes + 8 * cur : sc.nodes + 8 * (size_t)cur;
-      const F4 lx = g[0], hx = g[1], ly = g[2], hy = g[3], lz = g[4], hz = g[5], cc = g[6];
+      const F4 cc = g[0], lx = g[1], hx = g[2], ly = g[3], hy = g[4], lz = g[5], hz = g[6];
       const float tmax = tr.best.t;
       float tn[4];
       uint32_t ch[4];

@@ -261,6 +261,71 @@ K_BIN(k_max_u32, 0, uint32_t)
 K_BIN(k_or_b32, 0, uint32_t)
 #define OPS_k_lshl_add_u64 CH8("v_lshl_add_u64 %0, %0, 2, %1")
 
+#define OPS_k_lshl_add_u64 CH8("v_lshl_add_u64 %0, %0, 2, %1")
+__global__ void k_lshl_add_u64(uint32_t* out, uint32_t seed) {
+  uint64_t a[8];
+  uint64_t m = 0x12345ull ^ seed;
+  for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
+  for (int it = 0; it < ITERS; ++it) {
+#define OP(i) asm volatile("v_lshl_add_u64 %0, %0, 2, %1" : "+v"(a[i]) : "v"(m));
+    BODY8(OP)
+#undef OP
+  }
+  uint64_t s = 0;
+  for (int i = 0; i < 8; ++i) s ^= a[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)s;
+}
+__global__ void k_mov_b64(uint32_t* out, uint32_t seed) {
+  uint64_t a[8];
+  uint64_t m = 0x12345ull ^ seed;
+  for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
+  for (int it = 0; it < ITERS; ++it) {
+#define OP(i) asm volatile("v_mov_b64 %0, %1" : "=v"(a[i]) : "v"(m + i));
+    BODY8(OP)
+#undef OP
+  }
+  uint64_t s = 0;
+  for (int i = 0; i < 8; ++i) s ^= a[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)s;
+}
+__global__ void k_readlane(uint32_t* out, uint32_t seed) {
+  uint32_t a[8];
+  for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i + seed;
+  uint32_t acc = 0;
+  for (int it = 0; it < ITERS; ++it) {
+#define OP(i) { uint32_t r; asm volatile("v_readlane_b32 %0, %1, 3" : "=s"(r) : "v"(a[i])); acc += r; }
+    BODY8(OP)
+#undef OP
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+__global__ void k_writelane(uint32_t* out, uint32_t seed) {
+  uint32_t a[8];
+  for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
+  uint32_t sv = seed;
+  for (int it = 0; it < ITERS; ++it) {
+#define OP(i) asm volatile("v_writelane_b32 %0, %1, 5" : "+v"(a[i]) : "s"(sv));
+    BODY8(OP)
+#undef OP
+  }
+  uint32_t s = 0;
+  for (int i = 0; i < 8; ++i) s ^= a[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+#define OPS_k_cmp_eq_u32 CH8("v_cmp_eq_u32 vcc, %0, %1")
+K_BIN(k_cmp_eq_u32, 0, uint32_t)
+#define OPS_k_floor_f32 CH8("v_floor_f32 %0, %0")
+K_BIN(k_floor_f32, 0, float)
+#define OPS_k_cvt_u32_f32 CH8("v_cvt_u32_f32 %0, %0")
+K_BIN(k_cvt_u32_f32, 0, uint32_t)
+#define OPS_k_mbcnt CH8("v_mbcnt_lo_u32_b32 %0, -1, %0")
+K_BIN(k_mbcnt, 0, uint32_t)
+#define OPS_k_sub_u32 CH8("v_sub_u32 %0, %0, %1")
+K_BIN(k_sub_u32, 0, uint32_t)
+#define OPS_k_fmac_f32 CH8("v_fmac_f32 %0, %0, %1")
+K_BIN(k_fmac_f32, 0, float)
+#define OPS_k_pk_add_f32 CH8("v_pk_add_f32 %0, %0, %1")
+
 typedef void (*K)(uint32_t*, uint32_t);
 
 static void run(const char* name, K k, uint32_t* d) {
@@ -324,6 +389,16 @@ int main() {
   run("v_max3_f32", k_max3_f32, d);
   run("v_max_u32", k_max_u32, d);
   run("v_or_b32", k_or_b32, d);
+  run("v_lshl_add_u64", k_lshl_add_u64, d);
+  run("v_mov_b64", k_mov_b64, d);
+  run("v_readlane_b32", k_readlane, d);
+  run("v_writelane_b32", k_writelane, d);
+  run("v_cmp_eq_u32", k_cmp_eq_u32, d);
+  run("v_floor_f32", k_floor_f32, d);
+  run("v_cvt_u32_f32", k_cvt_u32_f32, d);
+  run("v_mbcnt_lo_u32_b32", k_mbcnt, d);
+  run("v_sub_u32", k_sub_u32, d);
+  run("v_fmac_f32", k_fmac_f32, d);
   hipFree(d);
   return 0;
 }
