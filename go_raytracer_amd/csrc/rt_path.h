@@ -123,6 +123,13 @@ RT_D void st_lds(F4* p, F4 v) { *(lds_v4*)p = v4f{v.x, v.y, v.z, v.w}; }
 RT_D void wait_vm() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 RT_D void st_glb(F4* p, F4 v) { *(glb_v4*)p = v4f{v.x, v.y, v.z, v.w}; }
 
+// m ? b : a, bitwise (v_bitop3_b32, truth table 0xD8 over (a, b, m)).  With m a sign mask
+// this is a select in one full-rate instruction: hipcc turns the same C expression into
+// v_cmp + v_cndmask, both of which issue at half rate or less on gfx950
+// (profiles/r4_instr_rate.jsonl)
+RT_D uint32_t pick_by(uint32_t a, uint32_t b, uint32_t m) { return __builtin_amdgcn_bitop3_b32(a, b, m, 0xD8); }
+// all ones when x < 0 (sign bit set), else 0: -0 and negative NaNs count as negative
+RT_D uint32_t neg_mask(float x) { return (uint32_t)((int32_t)__float_as_uint(x) >> 31); }
 RT_D uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
 // Debug build (-DRT_PHASES, tools/phase_probe.py): shader-clock cycles each wave
@@ -441,19 +448,24 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
           const float tz0 = (Nz[k] - o.z) * inv.z, tz1 = (Fz[k] - o.z) * inv.z;
           const float t0 = fmaxf(fmaxf(tx0, ty0), fmaxf(tz0, tmin));
           const float t1 = fminf(fminf(tx1, ty1), fminf(tz1, tmax));
-          // (an empty slot's inverted infinite box gives t1 = -inf: no code check)
-          const bool h = t0 <= t1 * 1.00000024f;  // slab() semantics
-          tn[k] = h ? t0 : kInf;
+          // hit when t0 <= t1 * (1 + 2 ulp) (slab() semantics), i.e. when that difference
+          // is not negative: tn = hit ? t0 : inf as a sign-mask select.  (An empty slot's
+          // inverted infinite box gives t1 = -inf: no code check.  t0 = t1 = inf gives a
+          // NaN difference with the sign clear: a "hit" at inf, as with the comparison.)
+          tn[k] = bitsf(pick_by(fbits(t0), 0x7F800000u, neg_mask(t1 * 1.00000024f - t0)));
           ch[k] = C[k];
         }
+        // compare-exchange as sign-mask selects: swap when tn[b] - tn[a] < 0, i.e. when
+        // tn[b] < tn[a] (the difference of two distinct floats is never +-0; inf - inf
+        // gives a NaN with the sign clear: no swap, like the comparison)
         auto cx = [&](int a, int b) {
-          const bool sw = tn[b] < tn[a];
-          const float ta = tn[a], tb = tn[b];
+          const uint32_t m = neg_mask(tn[b] - tn[a]);
+          const uint32_t ta = fbits(tn[a]), tb = fbits(tn[b]);
           const uint32_t ca = ch[a], cb = ch[b];
-          tn[a] = sw ? tb : ta;
-          tn[b] = sw ? ta : tb;
-          ch[a] = sw ? cb : ca;
-          ch[b] = sw ? ca : cb;
+          tn[a] = bitsf(pick_by(ta, tb, m));
+          tn[b] = bitsf(pick_by(tb, ta, m));
+          ch[a] = pick_by(ca, cb, m);
+          ch[b] = pick_by(cb, ca, m);
         };
         cx(0, 1);
         cx(2, 3);
