@@ -23,7 +23,7 @@ def main(argv):
     for src in srcs:
         cmd = ["/opt/rocm/bin/hipcc", "-DBRUTE_WAVES=6", "-O3", "-std=c++17", "--offload-arch=gfx950",
                "-I../../include", "-I.", "-Wno-unused-result",
-               "-fno-hip-fp32-correctly-rounded-divide-sqrt", "--cuda-device-only", "-c", src,
+               "-fno-hip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize", "--cuda-device-only", "-c", src,
                "-o", "/tmp/_kr.o", "-Rpass-analysis=kernel-resource-usage"] + extra + \
               (SETS_FLAGS if src == "rt_fused_sets.hip" else [])
         out += subprocess.run(cmd, cwd=CSRC, capture_output=True, text=True).stderr
