@@ -763,6 +763,27 @@ RT_D v2f pfma(v2f a, v2f b, v2f c) { return __builtin_elementwise_fma(a, b, c); 
 RT_D bool unit_ab(float a, float b) {
   return max(__float_as_uint(a), __float_as_uint(b)) <= 0x3F800000u;
 }
+// The record tests' acceptance as a sign mask (all ones = reject), from differences whose
+// sign bit says the same as each comparison: |den| - 1e-8, t - tmin, best - t (>= 0 when
+// the comparison holds; equal values give +0) and 1.0f's bits - max(alpha, beta bits)
+// (unit_ab).  Then the closest-hit update is two v_bitop3 selects instead of v_cmp /
+// v_cndmask (half rate and slower on gfx950, profiles/r4_instr_rate.jsonl): same choices.
+RT_D uint32_t rec_reject(float den, float t, float tmin, float best, float a, float b) {
+  const uint32_t ab = 0x3F800000u - max(__float_as_uint(a), __float_as_uint(b));
+  const uint32_t any = __builtin_amdgcn_bitop3_b32(__float_as_uint(fabsf(den) - 1e-8f),
+                                                   __float_as_uint(t - tmin),
+                                                   __float_as_uint(best - t), 0xFE) | ab;
+  return (uint32_t)((int32_t)any >> 31);
+}
+// the same without the denominator test (axis-aligned records: the inverse of the axis
+// direction component is NaN when |d_a| < 1e-8; a NaN t makes alpha and beta NaN, whose
+// bits exceed 1.0f's in either sign, so the alpha/beta term rejects it as t >= tmin did)
+RT_D uint32_t rec_reject_t(float t, float tmin, float best, float a, float b) {
+  const uint32_t ab = 0x3F800000u - max(__float_as_uint(a), __float_as_uint(b));
+  const uint32_t any = __builtin_amdgcn_bitop3_b32(__float_as_uint(t - tmin),
+                                                   __float_as_uint(best - t), ab, 0xFE);
+  return (uint32_t)((int32_t)any >> 31);
+}
 // one record pair's loop fields (7 x 16 B) from the LDS cache or the scalar cache
 template <bool SMEM>
 RT_D void load_pair(const DevScene& sc, const F4* lrec, int p, v4f r[7]) {
@@ -803,12 +824,12 @@ RT_D void brute_axis(const DevScene& sc, const F4* lrec, int p0, int p1, const v
     const v2f pc = pfma(Dv[B1], t, O[B1]) - pair_q<B1>(r);
     const v2f a = pfma(pc, pair_a<B1>(r), pb * pair_a<B0>(r));
     const v2f b = pfma(pc, pair_b<B1>(r), pb * pair_b<B0>(r));
-    const bool c0 = t.x >= tmin && unit_ab(a.x, b.x) && t.x <= best;
-    best = c0 ? t.x : best;
-    bk = c0 ? k0 : bk;
-    const bool c1 = t.y >= tmin && unit_ab(a.y, b.y) && t.y <= best;
-    best = c1 ? t.y : best;
-    bk = c1 ? k1 : bk;
+    const uint32_t m0 = rec_reject_t(t.x, tmin, best, a.x, b.x);
+    best = bitsf(pick_by(fbits(t.x), fbits(best), m0));
+    bk = pick_by(k0, bk, m0);
+    const uint32_t m1 = rec_reject_t(t.y, tmin, best, a.y, b.y);
+    best = bitsf(pick_by(fbits(t.y), fbits(best), m1));
+    bk = pick_by(k1, bk, m1);
   }
 }
 // Pairs parallel to axis AX (host-grouped): n_AX = 0 and A_AX = 0 exactly and B has only
@@ -834,12 +855,12 @@ RT_D void brute_vert(const DevScene& sc, const F4* lrec, int p0, int p1, const v
     const v2f p1v = pfma(Dv[B1], t, O[B1]) - pair_q<B1>(r);
     const v2f a = pfma(p1v, pair_a<B1>(r), p0v * pair_a<B0>(r));
     const v2f b = pa * pair_b<AX>(r);
-    const bool c0 = fabsf(den.x) >= 1e-8f && t.x >= tmin && unit_ab(a.x, b.x) && t.x <= best;
-    best = c0 ? t.x : best;
-    bk = c0 ? k0 : bk;
-    const bool c1 = fabsf(den.y) >= 1e-8f && t.y >= tmin && unit_ab(a.y, b.y) && t.y <= best;
-    best = c1 ? t.y : best;
-    bk = c1 ? k1 : bk;
+    const uint32_t m0 = rec_reject(den.x, t.x, tmin, best, a.x, b.x);
+    best = bitsf(pick_by(fbits(t.x), fbits(best), m0));
+    bk = pick_by(k0, bk, m0);
+    const uint32_t m1 = rec_reject(den.y, t.y, tmin, best, a.y, b.y);
+    best = bitsf(pick_by(fbits(t.y), fbits(best), m1));
+    bk = pick_by(k1, bk, m1);
   }
 }
 // Boxes rotated about y (host-detected: six records forming a box, rt_render.hip), two per
@@ -882,11 +903,14 @@ RT_D void brute_box(const DevScene& sc, const F4* lrec, int p0, int p1, const v2
       const float az0 = h ? tz0.y : tz0.x, az1 = h ? tz1.y : tz1.x;
       const float tn = fmaxf(fmaxf(fminf(ax0, ax1), fminf(ay0, ay1)), fminf(az0, az1));
       const float tf = fminf(fminf(fmaxf(ax0, ax1), fmaxf(ay0, ay1)), fmaxf(az0, az1));
-      const bool enter = tn >= tmin;
-      const float t = enter ? tn : tf;
-      const bool c = tn <= tf && t >= tmin && t <= best;
-      best = c ? t : best;
-      bk = c ? (kBoxCode | ((uint32_t)p << 2) | ((uint32_t)h << 1) | (enter ? 0u : 1u)) : bk;
+      // enter = tn >= tmin; t = enter ? tn : tf; accept = tn <= tf && t >= tmin && t <= best,
+      // all as sign masks and v_bitop3 selects (rec_reject)
+      const uint32_t leave = neg_mask(tn - tmin);
+      const float t = bitsf(pick_by(fbits(tn), fbits(tf), leave));
+      const uint32_t rej = (uint32_t)((int32_t)__builtin_amdgcn_bitop3_b32(
+                               fbits(tf - tn), fbits(t - tmin), fbits(best - t), 0xFE) >> 31);
+      best = bitsf(pick_by(fbits(t), fbits(best), rej));
+      bk = pick_by(kBoxCode | ((uint32_t)p << 2) | ((uint32_t)h << 1) | (leave & 1u), bk, rej);
     }
   }
 }
@@ -951,12 +975,12 @@ RT_D void trav_brute(const DevScene& sc, const F4* lrec, f3 o, f3 d, float time,
     const v2f pz = pfma(dz, t, oz) - r[3].xy;
     const v2f a = pfma(pz, r[4].zw, pfma(py, r[4].xy, px * r[3].zw));
     const v2f b = pfma(pz, r[6].xy, pfma(py, r[5].zw, px * r[5].xy));
-    const bool c0 = fabsf(den.x) >= 1e-8f && t.x >= tmin && unit_ab(a.x, b.x) && t.x <= best;
-    best = c0 ? t.x : best;
-    bk = c0 ? k0 : bk;
-    const bool c1 = fabsf(den.y) >= 1e-8f && t.y >= tmin && unit_ab(a.y, b.y) && t.y <= best;
-    best = c1 ? t.y : best;
-    bk = c1 ? k1 : bk;
+    const uint32_t m0 = rec_reject(den.x, t.x, tmin, best, a.x, b.x);
+    best = bitsf(pick_by(fbits(t.x), fbits(best), m0));
+    bk = pick_by(k0, bk, m0);
+    const uint32_t m1 = rec_reject(den.y, t.y, tmin, best, a.y, b.y);
+    best = bitsf(pick_by(fbits(t.y), fbits(best), m1));
+    bk = pick_by(k1, bk, m1);
   }
   const v2f O[3] = {ox, oy, oz}, Dv[3] = {dx, dy, dz};
   const int q = ng + nvy;
