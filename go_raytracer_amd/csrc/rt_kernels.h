@@ -355,6 +355,55 @@ RT_D bool hit_box_rec(const F4 r[4], f3 o, f3 d, float iy, float tmin, float tma
   return true;
 }
 
+// ---- the same tests, branch-free, returning a reject mask (all ones: no hit) -------
+// Each comparison of the boolean tests becomes the sign of a difference (>= 0 exactly when
+// the comparison holds, equal values giving +0), OR-ed and spread by an arithmetic shift:
+// full-rate v_sub / v_bitop3 / v_ashr instead of v_cmp + exec-mask branches (v_cmp issues
+// at half rate on gfx950 and the hazard s_nops before its v_cndmask, profiles/
+// r4_instr_rate.jsonl).  The same hits, except that an exactly -0.0 barycentric (reference:
+// accepted) is rejected, as the record loop already does (unit_ab).
+RT_D uint32_t sign_any3(float a, float b, float c) {
+  return __builtin_amdgcn_bitop3_b32(fbits(a), fbits(b), fbits(c), 0xFE);
+}
+RT_D uint32_t spread_sign(uint32_t x) { return (uint32_t)((int32_t)x >> 31); }
+// Triangle.Hit objects.go:408-461 (hit_tri_rec's arithmetic)
+RT_D uint32_t hit_tri_rec_m(const F4 r[4], f3 o, f3 d, float tmin, float tmax, float& t_out,
+                            float& u_out, float& v_out) {
+  const f3 e0 = xyz(r[1]), e1 = xyz(r[2]);
+  const f3 pvec = cross(d, e1);
+  const float det = dot(e0, pvec);
+  const float inv = rcp(det);
+  const f3 tvec = o - xyz(r[0]);
+  const float u = dot(tvec, pvec) * inv;
+  const f3 qvec = cross(tvec, e0);
+  const float v = dot(d, qvec) * inv;
+  const float t = dot(e1, qvec) * inv;
+  t_out = t;
+  u_out = u;
+  v_out = v;
+  // |det| >= 1e-8, 0 <= u <= 1, v >= 0, u + v <= 1, tmin <= t <= tmax
+  const uint32_t a = sign_any3(fabsf(det) - 1e-8f, u, 1.0f - u);
+  const uint32_t b = sign_any3(v, 1.0f - (u + v), t - tmin);
+  return spread_sign(__builtin_amdgcn_bitop3_b32(a, b, fbits(tmax - t), 0xFE));
+}
+// quad.Hit objects.go:167-196 (hit_quad_rec's arithmetic)
+RT_D uint32_t hit_quad_rec_m(const F4 r[4], f3 o, f3 d, float tmin, float tmax, float& t_out,
+                             float& a_out, float& b_out) {
+  const F4 Q = r[0], N = r[1], A = r[2], B = r[3];
+  const f3 n = xyz(N);
+  const float denom = dot(n, d);
+  const float t = (N.w - dot(n, o)) * rcp(denom);
+  const f3 pp = (o + d * t) - xyz(Q);
+  const float alpha = dot(pp, xyz(A)), beta = dot(pp, xyz(B));
+  t_out = t;
+  a_out = alpha;
+  b_out = beta;
+  // |n.d| >= 1e-8, tmin <= t <= tmax, 0 <= alpha, beta <= 1 (unit_ab)
+  const uint32_t ab = 0x3F800000u - max(fbits(alpha), fbits(beta));
+  const uint32_t x = sign_any3(fabsf(denom) - 1e-8f, t - tmin, tmax - t);
+  return spread_sign(x | ab);
+}
+
 #define HAS(f) ((FT & (f)) != 0u)
 template <uint32_t FT>
 RT_D bool hit_record(const F4 r[4], f3 o, f3 d, float iy, float time, float tmin, float tmax,
@@ -371,6 +420,23 @@ RT_D bool hit_record(const F4 r[4], f3 o, f3 d, float iy, float time, float tmin
     return hit_tri_rec(r, o, d, tmin, tmax, t, u, v);
   u = v = 0.0f;
   return hit_sphere_rec(r, o, d, time, tmin, tmax, t);
+}
+
+// hit_record as a reject mask (the traversal's closest-hit update is then v_bitop3 selects)
+template <uint32_t FT>
+RT_D uint32_t hit_record_m(const F4 r[4], f3 o, f3 d, float iy, float time, float tmin, float tmax,
+                           float& t, float& u, float& v, uint32_t& ref) {
+  ref = fbits(r[0].w);
+  const uint32_t type = ref >> 30;
+  if (HAS(FT_BOX) && type == PRIM_BOX) {
+    u = -1.0f;
+    v = 0.0f;
+    return hit_box_rec(r, o, d, iy, tmin, tmax, t, ref) ? 0u : ~0u;
+  }
+  if (!HAS(FT_SPHERE | FT_TRI) || type == PRIM_QUAD) return hit_quad_rec_m(r, o, d, tmin, tmax, t, u, v);
+  if (HAS(FT_TRI) && (!HAS(FT_SPHERE) || type == PRIM_TRI)) return hit_tri_rec_m(r, o, d, tmin, tmax, t, u, v);
+  u = v = 0.0f;
+  return hit_sphere_rec(r, o, d, time, tmin, tmax, t) ? 0u : ~0u;
 }
 
 // same, with fp64 interval bounds and result (medium boundaries: the reference

@@ -503,12 +503,11 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
         for (uint32_t k = 0;;) {
           float t, u, vv;
           uint32_t ref;
-          if (hit_record<FT>(rec, o, d, inv.y, time, tmin, tr.best.t, t, u, vv, ref)) {
-            tr.best.t = t;
-            tr.best.u = u;
-            tr.best.v = vv;
-            tr.best.ref = ref;
-          }
+          const uint32_t rej = hit_record_m<FT>(rec, o, d, inv.y, time, tmin, tr.best.t, t, u, vv, ref);
+          tr.best.t = bitsf(pick_by(fbits(t), fbits(tr.best.t), rej));
+          tr.best.u = bitsf(pick_by(fbits(u), fbits(tr.best.u), rej));
+          tr.best.v = bitsf(pick_by(fbits(vv), fbits(tr.best.v), rej));
+          tr.best.ref = pick_by(ref, tr.best.ref, rej);
           if (++k >= count) break;
           const F4* q = sc.leafprims + 4 * (size_t)(first + k);
           for (int e = 0; e < 4; ++e) rec[e] = ld_glb(q + e);
@@ -599,12 +598,11 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
         }
         float t, u, v;
         uint32_t ref;
-        if (hit_record<FT>(rec, o, d, inv.y, time, tmin, tr.best.t, t, u, v, ref)) {
-          tr.best.t = t;
-          tr.best.u = u;
-          tr.best.v = v;
-          tr.best.ref = ref;
-        }
+        const uint32_t rej = hit_record_m<FT>(rec, o, d, inv.y, time, tmin, tr.best.t, t, u, v, ref);
+        tr.best.t = bitsf(pick_by(fbits(t), fbits(tr.best.t), rej));
+        tr.best.u = bitsf(pick_by(fbits(u), fbits(tr.best.u), rej));
+        tr.best.v = bitsf(pick_by(fbits(v), fbits(tr.best.v), rej));
+        tr.best.ref = pick_by(ref, tr.best.ref, rej);
       }
     }
     if (sp == 0) {
@@ -723,12 +721,11 @@ RT_D int trav_steps8(const DevScene& sc, const TravStack& stack, f3 o, f3 d, flo
       for (uint32_t k = 0;;) {
         float t, u, vv;
         uint32_t ref;
-        if (hit_record<FT>(rec, o, d, inv.y, time, tmin, tr.best.t, t, u, vv, ref)) {
-          tr.best.t = t;
-          tr.best.u = u;
-          tr.best.v = vv;
-          tr.best.ref = ref;
-        }
+        const uint32_t rej = hit_record_m<FT>(rec, o, d, inv.y, time, tmin, tr.best.t, t, u, vv, ref);
+        tr.best.t = bitsf(pick_by(fbits(t), fbits(tr.best.t), rej));
+        tr.best.u = bitsf(pick_by(fbits(u), fbits(tr.best.u), rej));
+        tr.best.v = bitsf(pick_by(fbits(vv), fbits(tr.best.v), rej));
+        tr.best.ref = pick_by(ref, tr.best.ref, rej);
         if (++k >= count) break;
         const F4* q = sc.recs8 + 4 * (size_t)(first + k);
         for (int e = 0; e < 4; ++e) rec[e] = ld_glb(q + e);
