@@ -366,6 +366,13 @@ RT_D uint32_t sign_any3(float a, float b, float c) {
   return __builtin_amdgcn_bitop3_b32(fbits(a), fbits(b), fbits(c), 0xFE);
 }
 RT_D uint32_t spread_sign(uint32_t x) { return (uint32_t)((int32_t)x >> 31); }
+// !unit_ab(a, b) in the sign bit: with m = max(bits(a), bits(b)), m > 1.0f's bits exactly
+// when (1.0f's bits - m) wraps negative (m in (0x3F800000, 0xBF800000]) or m itself has the
+// sign set (values below -1 and negative NaNs, where the difference wraps back positive)
+RT_D uint32_t unit_ab_rej(float a, float b) {
+  const uint32_t m = max(__float_as_uint(a), __float_as_uint(b));
+  return (0x3F800000u - m) | m;
+}
 // Triangle.Hit objects.go:408-461 (hit_tri_rec's arithmetic)
 RT_D uint32_t hit_tri_rec_m(const F4 r[4], f3 o, f3 d, float tmin, float tmax, float& t_out,
                             float& u_out, float& v_out) {
@@ -399,7 +406,7 @@ RT_D uint32_t hit_quad_rec_m(const F4 r[4], f3 o, f3 d, float tmin, float tmax, 
   a_out = alpha;
   b_out = beta;
   // |n.d| >= 1e-8, tmin <= t <= tmax, 0 <= alpha, beta <= 1 (unit_ab)
-  const uint32_t ab = 0x3F800000u - max(fbits(alpha), fbits(beta));
+  const uint32_t ab = unit_ab_rej(alpha, beta);
   const uint32_t x = sign_any3(fabsf(denom) - 1e-8f, t - tmin, tmax - t);
   return spread_sign(x | ab);
 }

@@ -762,11 +762,11 @@ RT_D bool unit_ab(float a, float b) {
 }
 // The record tests' acceptance as a sign mask (all ones = reject), from differences whose
 // sign bit says the same as each comparison: |den| - 1e-8, t - tmin, best - t (>= 0 when
-// the comparison holds; equal values give +0) and 1.0f's bits - max(alpha, beta bits)
-// (unit_ab).  Then the closest-hit update is two v_bitop3 selects instead of v_cmp /
-// v_cndmask (half rate and slower on gfx950, profiles/r4_instr_rate.jsonl): same choices.
+// the comparison holds; equal values give +0) and unit_ab_rej.  Then the closest-hit update
+// is two v_bitop3 selects instead of v_cmp / v_cndmask (half rate and slower on gfx950,
+// profiles/r4_instr_rate.jsonl): same choices.
 RT_D uint32_t rec_reject(float den, float t, float tmin, float best, float a, float b) {
-  const uint32_t ab = 0x3F800000u - max(__float_as_uint(a), __float_as_uint(b));
+  const uint32_t ab = unit_ab_rej(a, b);
   const uint32_t any = __builtin_amdgcn_bitop3_b32(__float_as_uint(fabsf(den) - 1e-8f),
                                                    __float_as_uint(t - tmin),
                                                    __float_as_uint(best - t), 0xFE) | ab;
@@ -776,7 +776,7 @@ RT_D uint32_t rec_reject(float den, float t, float tmin, float best, float a, fl
 // direction component is NaN when |d_a| < 1e-8; a NaN t makes alpha and beta NaN, whose
 // bits exceed 1.0f's in either sign, so the alpha/beta term rejects it as t >= tmin did)
 RT_D uint32_t rec_reject_t(float t, float tmin, float best, float a, float b) {
-  const uint32_t ab = 0x3F800000u - max(__float_as_uint(a), __float_as_uint(b));
+  const uint32_t ab = unit_ab_rej(a, b);
   const uint32_t any = __builtin_amdgcn_bitop3_b32(__float_as_uint(t - tmin),
                                                    __float_as_uint(best - t), ab, 0xFE);
   return (uint32_t)((int32_t)any >> 31);
@@ -1387,6 +1387,10 @@ struct SampleAcc {
     }
     const unsigned long long fx = to_fixed(L.x), fy = to_fixed(L.y), fz = to_fixed(L.z);
     if (lds) {
+#ifdef RT_ABLATE_ACC  // timing ablation only (wrong images): no per-sample LDS adds
+      if (fx == 0x1234567ull) __atomic_fetch_add((lds_u64*)lds, fx, __ATOMIC_RELAXED);
+      return;
+#endif
       __atomic_fetch_add((lds_u64*)lds, fx, __ATOMIC_RELAXED);
       __atomic_fetch_add((lds_u64*)lds + 256, fy, __ATOMIC_RELAXED);
       __atomic_fetch_add((lds_u64*)lds + 512, fz, __ATOMIC_RELAXED);
@@ -1405,7 +1409,12 @@ struct SampleAcc {
       lds_u64* q = (lds_u64*)lds + ch * 256;
       const unsigned long long s = *q;
       *q = 0ull;
-      if (s) atomicAdd(&P.accum[(size_t)ch * P.npix + lp], s);
+#ifdef RT_ABLATE_FLUSH  // timing ablation only (wrong images): no global pixel atomics
+      if (s == 0x1234567ull)
+#else
+      if (s)
+#endif
+        atomicAdd(&P.accum[(size_t)ch * P.npix + lp], s);
     }
   }
 };

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Bitwise A/B of two library builds (dev tool): renders small versions of every demo
 scene with the in-tree library and with RT_AMD_LIB=<other> (a child process) and
-reports whether the images are identical.  usage: tools/ab_bitwise.py OTHER.so"""
+reports whether the images are identical.  usage: tools/ab_bitwise.py OTHER.so [BASE.so]
+(BASE.so, if given, replaces the in-tree library on the first side)"""
 import json
 import os
 import subprocess
@@ -33,7 +34,11 @@ if __name__ == "__main__":
         render_all(sys.argv[2])
         sys.exit(0)
     other = os.path.abspath(sys.argv[1])
-    subprocess.run([sys.executable, __file__, "--render", "/tmp/ab_cur.npz"], check=True)
+    base_env = dict(os.environ)
+    if len(sys.argv) > 2:
+        base_env["RT_AMD_LIB"] = os.path.abspath(sys.argv[2])
+    subprocess.run([sys.executable, __file__, "--render", "/tmp/ab_cur.npz"], check=True,
+                   env=base_env)
     subprocess.run([sys.executable, __file__, "--render", "/tmp/ab_other.npz"], check=True,
                    env=dict(os.environ, RT_AMD_LIB=other))
     a, b = np.load("/tmp/ab_cur.npz"), np.load("/tmp/ab_other.npz")

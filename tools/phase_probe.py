@@ -3,7 +3,8 @@
 built with -DRT_PHASES (tools/build_variant.sh phases -DRT_PHASES; run with
 RT_AMD_LIB=go_raytracer_amd/build_abl/phases/librt_amd.so).
 usage: phase_probe.py scene width spp  -> one JSON line: phase shares of the loop's
-cycles, traversal/shading lane utilisation"""
+cycles, traversal/shading lane utilisation.  CHUNK=K fixes the chunk size, NRANKS=N renders
+rank 0's row share of N"""
 import json
 import os
 import sys
@@ -26,12 +27,14 @@ with rt.Scene(t, w, l) as sc:
     sc.render(cam)
     cam.SamplesPerPixel = spp
     os.environ["RT_WAVE_TIMES"] = path
-    img, st = sc.render(cam, profile=True)
+    kw = {"chunk": int(os.environ["CHUNK"])} if "CHUNK" in os.environ else {}
+    img, st = sc.render(cam, profile=True, nranks=int(os.environ.get("NRANKS", "1")), **kw)
     os.environ.pop("RT_WAVE_TIMES")
 a = np.fromfile(path, dtype=np.uint64).reshape(-1, 18).astype(np.float64)
 ph = a[:, 4:].sum(axis=0)
 loop = ph[7]
 out = {"scene": scene, "W": width, "spp": spp, "ms": round(st["ms_fused"], 2),
+       "chunk": st.get("chunk_samples"), "nranks": int(os.environ.get("NRANKS", "1")),
        "segments": st["segments"], "waves": len(a)}
 for i in range(7):
     out[NAMES[i]] = round(ph[i] / loop, 4)
