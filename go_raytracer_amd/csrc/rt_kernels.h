@@ -250,6 +250,22 @@ RT_D bool hit_prim(const DevScene& sc, uint32_t ref, f3 o, f3 d, float time, flo
 RT_D bool hit_sphere_rec(const F4 r[4], f3 o, f3 d, float time, float tmin, float tmax,
                          float& t_out) {
   const F4 c0 = r[0], mv = r[1];
+#ifdef RT_ABLATE_SPHERE32  // timing ablation only (the naive fp32 quadratic; not the product)
+  {
+    const f3 oc = mk3(c0.x + time * mv.x, c0.y + time * mv.y, c0.z + time * mv.z) - o;
+    const float a = dot(d, d), h = dot(d, oc), cc = dot(oc, oc) - mv.w * mv.w;
+    const float disc = h * h - a * cc;
+    if (disc < 0.0f) return false;
+    const float sq = fsqrt(disc), ia = rcp(a);
+    float root = (h - sq) * ia;
+    if (!(tmin < root && root < tmax)) {
+      root = (h + sq) * ia;
+      if (!(tmin < root && root < tmax)) return false;
+    }
+    t_out = root;
+    return true;
+  }
+#endif
   double cx = (double)c0.x + (double)time * (double)mv.x;
   double cy = (double)c0.y + (double)time * (double)mv.y;
   double cz = (double)c0.z + (double)time * (double)mv.z;

@@ -1247,6 +1247,7 @@ RT_D float prim_pdf(const DevScene& sc, uint32_t ref, int li, f3 origin, f3 dir)
   }
   float t, u, v, area;
   f3 n;
+  uint32_t miss = 0u;  // quad lights: the reject mask of the branch-free test
   if (!HAS(FT_TRI) || type == PRIM_QUAD) {
     // the light's leaf-record copy (uniform index: scalar loads) and the traversal's quad test
     F4 rec[4];
@@ -1257,7 +1258,7 @@ RT_D float prim_pdf(const DevScene& sc, uint32_t ref, int li, f3 origin, f3 dir)
       const F4* lr = sc.light_recs + 8 * (size_t)li;
       rec[0] = lr[0], rec[1] = lr[1], rec[2] = lr[2], rec[3] = lr[3];
     }
-    if (!hit_quad_rec(rec, origin, dir, 0.001f, kInf, t, u, v)) return 0.0f;
+    miss = hit_quad_rec_m(rec, origin, dir, 0.001f, kInf, t, u, v);
     n = xyz(rec[1]);
     area = rec[2].w;
   } else {
@@ -1265,9 +1266,10 @@ RT_D float prim_pdf(const DevScene& sc, uint32_t ref, int li, f3 origin, f3 dir)
     n = tri_normal(sc, idx, u, v);
     area = sc.tri[3 * (size_t)idx + 1].w;
   }
-  // dist2 / (cosine * area) with dist2 = t^2 |dir|^2, cosine = |dir.n| / |dir|
+  // dist2 / (cosine * area) with dist2 = t^2 |dir|^2, cosine = |dir.n| / |dir|; +0 on a
+  // miss (the mask clears every bit of whatever the missed test's t gave)
   const float dd = dot(dir, dir);
-  return (t * t * dd) * fsqrt(dd) * rcp(fabsf(dot(dir, n)) * area);
+  return bitsf(fbits((t * t * dd) * fsqrt(dd) * rcp(fabsf(dot(dir, n)) * area)) & ~miss);
 }
 
 // HittableList.PdfValue hittable.go:89-97 over the flattened light table
@@ -1414,7 +1416,11 @@ struct SampleAcc {
 #else
       if (s)
 #endif
+#ifdef RT_ABLATE_STFLUSH  // timing ablation only (wrong images): plain stores, not atomics
+        P.accum[(size_t)ch * P.npix + lp] = s;
+#else
         atomicAdd(&P.accum[(size_t)ch * P.npix + lp], s);
+#endif
     }
   }
 };
