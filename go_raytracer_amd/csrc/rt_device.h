@@ -193,7 +193,10 @@ struct DevScene {
   int32_t merge_ok;     // every weight and radiance is >= 0 (solid colours, metal albedos
                         // and, per render, the background): dominated clamp vertices may
                         // be merged (rt_path.h shade_core); else each vertex is pushed
-  int32_t _pad_sc;
+  int32_t shade_lds;    // record-loop kernel of the lean set: F4 offset of the quads' shade
+                        // table in the dynamic LDS (after the record pairs), or -1
+  int32_t shade_n;      // F4s of that table (2 per quad: normal | kind, solid colour)
+  int32_t _pad_sc2;
 };
 
 }  // namespace rt

@@ -13,9 +13,11 @@ RT_D bool stage_nodes(const Params& P, F4* lnodes, int W) {
   const int nl = min(P.sc.n_nodes, 4 * kLdsNodes / W);
   for (int i = threadIdx.x; i < W * nl; i += blockDim.x) lnodes[i] = P.sc.nodes[i];
   const bool recs = P.recs_lds != 0u;
-  if (recs)
-    for (int i = threadIdx.x; i < 4 * P.sc.n_refs; i += blockDim.x)
-      lnodes[W * nl + i] = P.sc.leafprims[i];
+  if (recs) {
+    // + the lean set's shade table after the record pairs (rt_render.hip)
+    const int n = 4 * P.sc.n_refs + (P.sc.shade_lds >= 0 ? P.sc.shade_n : 0);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) lnodes[W * nl + i] = P.sc.leafprims[i];
+  }
   __syncthreads();
   return recs;
 }

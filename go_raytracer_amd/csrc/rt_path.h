@@ -201,6 +201,8 @@ RT_D Ids chunk_ids(const Params& P, uint32_t chunk) {
 // VGPR lanes, one v_readlane per use).  [0] pixel00 - center | 1/s, [1] du | fd_s.m,
 // [2] dv | fd_s shifts, [3] center | s, [4] defocus u | defocus flag, [5] defocus v.
 __shared__ F4 g_cam[6];
+// the dynamic LDS of the fused kernels (k_fused's lnodes: tree, records, shade table)
+extern __shared__ F4 g_dyn_lds[];
 // Kernels that read the camera from g_cam (round 2, against SGPR-resident constants): the
 // book2 and mesh sets (C4 -3.6 %, C5 -2.3 %, fewer SGPR and VGPR spills); the C2 and C3
 // kernels lost from it (their VGPR budget takes the loaded constants: C2 +26 %)
@@ -1642,6 +1644,10 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
   bool ff = true;
   DevMaterial M;
   bool scat = false;
+  // lean record-loop kernel: the quad's normal, material kind and solid colour from the
+  // shade table in LDS (rt_render.hip), no global loads
+  bool ltab = false;
+  f3 lcol = mk3(0, 0, 0);
   if (ref != PRIM_NONE) {
     const float t = h.t;
     p = o + d * t;  // r.At(t)
@@ -1663,6 +1669,15 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
         u = phi * (0.5f * kInvPi);
         v = theta * kInvPi;
       }
+    } else if (FT == 0u && sc.shade_lds >= 0) {
+      const F4* tab = g_dyn_lds + sc.shade_lds + 2 * idx;
+      const F4 a = ld_lds(tab);
+      lcol = xyz(ld_lds(tab + 1));
+      nout = xyz(a);
+      mat = (int)fbits(a.w);  // the material KIND here
+      ltab = true;
+      ff = dot(d, nout) < 0;
+      n = ff ? nout : -nout;
     } else if (!HAS(FT_TRI | FT_MEDIA) || type == PRIM_QUAD) {
       const F4* q = sc.quad + 5 * (size_t)idx;
       nout = xyz(q[3]);
@@ -1700,7 +1715,10 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
       ff = true;
       u = v = 0.0f;
     }
-    M = sc.mats[mat];
+    if (ltab)
+      M.kind = mat;
+    else
+      M = sc.mats[mat];
     scat = M.kind != RT_MAT_DIFFUSE_LIGHT;
   }
   // ONE Philox call per vertex for the whole wave: a scattering vertex draws its
@@ -1717,7 +1735,7 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
     if (ref == PRIM_NONE)
       lterm = mk3(P.bg[0], P.bg[1], P.bg[2]);  // camera.go:300-302
     else  // Emitted materials.go:150-155; Scatter false
-      lterm = ff ? tex_value<FT>(sc, M.tex, u, v, p) : mk3(0, 0, 0);
+      lterm = ff ? (ltab ? lcol : tex_value<FT>(sc, M.tex, u, v, p)) : mk3(0, 0, 0);
     term = true;
     if (kMergeDraws) {
       rcam = r;
@@ -1752,7 +1770,7 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
       } else {  // lambertian materials.go:45-57 / isotropic :157-177 + mixture pdf.go:58-74
         const bool iso = HAS(FT_MEDIA) && M.kind == RT_MAT_ISOTROPIC;
         PH_T(t_tex);
-        f3 att = tex_value<FT>(sc, M.tex, u, v, p);
+        f3 att = ltab ? lcol : tex_value<FT>(sc, M.tex, u, v, p);
         PH_ADD(PH_TEX, t_tex);
         PH_T(t_light);
         Onb b;

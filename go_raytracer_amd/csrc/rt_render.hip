@@ -181,6 +181,7 @@ struct DeviceScene {
   const F4* nodes2 = nullptr;   // BVH2 of the same leaves (tiny scenes)
   const F4* brute_pairs = nullptr;  // quad records in pairs, largest first (record loop)
   size_t brute_slots = 0;           // records in brute_pairs, pads included (even)
+  int32_t shade_n = 0;              // F4s of the lean shade table after the pairs (0: none)
   int32_t brute_boxes = 0;          // boxes among them tested as slabs (rt_path.h brute_box)
   uint32_t root2 = PRIM_NONE;
   int32_t n_nodes2 = 0;
@@ -685,6 +686,35 @@ static int upload_scene(const Scene* s, DeviceScene* ds) {
       for (int e = 0; e < 15; ++e) f[2 * e] = v[e];
     }
     ds->brute_slots = slots.size();
+    // The lean set's shade table, after the pairs: per quad its normal and material kind,
+    // and its texture's solid colour (2 F4), so the record-loop kernel shades from LDS
+    // instead of three dependent global loads (quad, material, texture) per vertex, whose
+    // s_waitcnt vmcnt(0) also waited for the chunk flushes' pixel atomics
+    // (profiles/r4_phases_flush_c2.jsonl).  Only when every quad's material is Lambertian
+    // or a diffuse light with a solid texture (what the lean kernel shades).
+    {
+      const size_t nq = h.quad.size() / 5;
+      std::vector<F4> tab(2 * nq);
+      bool ok = nq > 0;
+      for (size_t qi = 0; qi < nq && ok; ++qi) {
+        const F4* q = &h.quad[5 * qi];
+        uint32_t mb;
+        memcpy(&mb, &q[2].w, 4);
+        ok = mb < mats.size();
+        if (!ok) break;
+        const DevMaterial& m = mats[mb];
+        ok = (m.kind == RT_MAT_LAMBERTIAN || m.kind == RT_MAT_DIFFUSE_LIGHT) && m.tex >= 0 &&
+             (size_t)m.tex < h.texs.size() && h.texs[m.tex].kind == RT_TEX_SOLID;
+        if (!ok) break;
+        float kb;
+        const uint32_t kind = (uint32_t)m.kind;
+        memcpy(&kb, &kind, 4);
+        tab[2 * qi] = {q[3].x, q[3].y, q[3].z, kb};
+        tab[2 * qi + 1] = h.texs[m.tex].color;
+      }
+      ds->shade_n = ok && env_int("RT_SHADE_LDS", 1) != 0 ? (int32_t)tab.size() : 0;
+      if (ds->shade_n) pairs.insert(pairs.end(), tab.begin(), tab.end());
+    }
     if ((rc = upload(ds, pairs, &ds->brute_pairs)) != RT_OK) return rc;
   }
 records_done:
@@ -712,6 +742,8 @@ records_done:
   // the weight merge needs non-negative suffix products: every texture value (solid
   // colours; image and noise values are >= 0 by construction) and metal albedo >= 0
   // (the background is checked per render)
+  d.shade_lds = -1;  // set per launch (record-loop kernel with the records in LDS)
+  d.shade_n = 0;
   d.merge_ok = 1;
   for (const auto& t : h.texs)
     if (t.kind == RT_TEX_SOLID && !(t.color.x >= 0.0f && t.color.y >= 0.0f && t.color.z >= 0.0f))
@@ -905,7 +937,9 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   const size_t n_nodes = tree == 4 ? s->h.nodes4.size() / 8 : tree == 2 ? s->h.nodes.size() / 4 : 0;
   const size_t node_slots = w4 ? 2 : 1;  // 64-B LDS slots per node
   const bool f_lds = node_slots * n_nodes <= lds_slots && !brute_smem;
-  const size_t rec_slots = tree == 0 ? brute_slots : n_refs;
+  // the record loop's pairs, then (lean set) the quads' shade table, 4 F4 per 64-B slot
+  const bool shade_tab = tree == 0 && ft_set == 0u && ds->shade_n > 0;
+  const size_t rec_slots = tree == 0 ? brute_slots + (shade_tab ? (size_t)(ds->shade_n + 3) / 4 : 0) : n_refs;
   const bool f_recs = f_lds && node_slots * n_nodes + rec_slots <= lds_slots;
   // Trees read through L1/L2 take the BVH8 (host_bvh8.cpp) when the scene has one (built
   // only with RT_BVH8=1) and a kernel exists for its feature set; RT_TREE=4 keeps the BVH4
@@ -990,6 +1024,10 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     p.sc.n_nodes = 0;  // records only (stage_nodes puts them at the start of the cache)
     p.sc.leafprims = ds->brute_pairs;
     p.sc.n_refs = (int32_t)brute_slots;  // even: whole pairs
+    if (shade_tab && f_recs) {  // the shade table follows the pairs, in LDS as in HBM
+      p.sc.shade_lds = (int32_t)(4 * brute_slots);
+      p.sc.shade_n = ds->shade_n;
+    }
   }
   for (int i = 0; i < 3; ++i) {
     p.p00r[i] = (float)(cd.pixel00[i] - cd.center[i]);
