@@ -149,6 +149,20 @@ __global__ __launch_bounds__(256) void k_resolve(Params P, float* out, double sc
   const uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
   if (lp >= P.npix) return;
   const uint32_t f = P.pflags[lp];
+  // the fused kernel's per-chunk sums (SampleAcc::flush): this pixel's chunks are
+  // q * gchunks + sub * gpix + r for its group q, its place r in the group and every
+  // sample block sub (chunk_pixel), summed mod 2^64 like the atomics they replace
+  unsigned long long cs[3] = {0ull, 0ull, 0ull};
+  if (P.csum) {
+    const uint32_t gpix = P.fd_gpix.d, q = fdiv(lp, P.fd_gpix), r = lp - q * gpix;
+    const uint32_t cpp = P.fd_gchunks.d / gpix;
+    const unsigned long long* rec = P.csum + 4 * ((size_t)q * P.fd_gchunks.d + r);
+    for (uint32_t sb = 0; sb < cpp; ++sb, rec += 4 * (size_t)gpix) {
+      cs[0] += rec[0];
+      cs[1] += rec[1];
+      cs[2] += rec[2];
+    }
+  }
   for (int ch = 0; ch < 3; ++ch) {
     const bool nan = (f & (1u << ch)) != 0, pinf = (f & (8u << ch)) != 0,
                ninf = (f & (64u << ch)) != 0;
@@ -159,7 +173,7 @@ __global__ __launch_bounds__(256) void k_resolve(Params P, float* out, double sc
       v = pinf ? kInf : -kInf;
     } else {
       const size_t i = (size_t)ch * P.npix + lp;
-      const long long sum = (long long)P.accum[i];
+      const long long sum = (long long)(P.accum[i] + cs[ch]);
       v = (float)(((double)sum * 2.3283064365386963e-10 + P.side[i]) * scale);
     }
     out[3 * (size_t)lp + ch] = v;
@@ -203,6 +217,8 @@ struct RenderState {
   uint32_t* queue[2] = {nullptr, nullptr};
   Counters* ctr = nullptr;
   unsigned long long* accum = nullptr;
+  unsigned long long* csum = nullptr;  // fused: per-chunk sums (4 x u64 per chunk)
+  size_t csum_chunks = 0;
   double* side = nullptr;
   uint32_t* pflags = nullptr;
   uint32_t* ostack = nullptr;
@@ -955,8 +971,12 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     P = (uint32_t)fused_blocks * 256u;
   }
   // Samples per chunk.  Fused: the largest K in {32, 16, 8} that still gives
-  // every lane >= 48 chunks (tree in LDS) or >= 100 (tree through L1/L2, whose
+  // every lane >= 12 chunks (tree in LDS) or >= 100 (tree through L1/L2, whose
   // per-pixel cost varies more), so the last chunks do not leave most lanes idle.
+  // Round 4 (partitioned counters, chunk sums as plain stores): C2's 2-, 4- and 8-GPU
+  // shares are fastest at K = 32 / 16 / 16 (16.9 / 8.67 / 4.68 ms; K = 8: 18.2 / 9.03 /
+  // 4.91, profiles/r4_chunk_probe_csum.jsonl), which 12 chunks per lane picks; 48 picked
+  // 16 / 8 / 8.
   // Measured with the row-group order (tools/chunk_probe.py,
   // profiles/r2_chunk_size_*.jsonl): 8-GPU shares of C2/C3/C4/C5 are fastest at
   // K = 8 (C5 -27 % against 32), whole images at K = 32 (C3 -3 % against 8); at 100
@@ -965,7 +985,7 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   if (o.chunk > 0) {
     K = (uint32_t)o.chunk;
   } else if (mode == RT_MODE_FUSED) {
-    const uint64_t work = (uint64_t)npix * ss, need = (uint64_t)(f_lds ? 48u : 100u) * P;
+    const uint64_t work = (uint64_t)npix * ss, need = (uint64_t)(f_lds ? 12u : 100u) * P;
     K = f_lds ? 8u : 4u;  // the smallest: C3's 8-GPU share 6 % faster at 4 than 8 (C2's ±1 %)
     for (uint32_t k : {32u, 16u, 8u})
       if (work / k >= need) {
@@ -1004,6 +1024,17 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
       if ((rc = dalloc(st, &st->ostack, (size_t)(kStack - kShortStackMin) * cols))) return rc;
       st->ostack_cols = cols;
     }
+  }
+  // fused: the per-chunk sums (32 B per chunk, every record stored once per render: no clear)
+  const bool use_csum = mode == RT_MODE_FUSED && env_int("RT_CSUM", 1) != 0;
+  if (use_csum && st->csum_chunks < n_chunks) {
+    if (st->csum) {
+      HIP_OK(hipFree(st->csum));
+      st->allocs.erase(std::find(st->allocs.begin(), st->allocs.end(), (void*)st->csum));
+      st->csum = nullptr;
+    }
+    if ((rc = dalloc(st, &st->csum, 4 * (size_t)n_chunks))) return rc;
+    st->csum_chunks = n_chunks;
   }
 
   hipStream_t stream = (hipStream_t)o.stream;
@@ -1106,6 +1137,7 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   p.queue[1] = st->queue[1];
   p.ctr = st->ctr;
   p.accum = st->accum;
+  p.csum = use_csum ? st->csum : nullptr;
   p.side = st->side;
   // |v| < 2^31 / ss: the ss-sample fixed-point sum of a pixel stays inside int64
   p.vlim = std::nextafter((float)(2147483648.0 / (double)std::max<uint32_t>(ss, 1u)), 0.0f);
