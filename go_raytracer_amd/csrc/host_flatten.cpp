@@ -122,6 +122,7 @@ struct Flattener {
   };
   std::vector<BoxLeaf> box_leaves;
   bool box_leaves_on = true;
+  double big_r = kBigSphereR;  // spheres at least this large: out.big_refs
 
   explicit Flattener(const Tree& tr, HostScene& o) : t(tr), out(o) {
     has_med.assign(t.nodes.size(), -1);
@@ -462,7 +463,10 @@ struct Flattener {
         if (role == 0) {
           D3 mn, mx;
           uint32_t ref = emit_prim(n, xf, &mn, &mx);
-          add_bounds(ref, mn, mx);
+          if (n.kind == RT_NODE_SPHERE && fabs(n.p[6]) >= big_r)
+            out.big_refs.push_back(ref);  // tested before the BVH, in fp64 (trav_init)
+          else
+            add_bounds(ref, mn, mx);
         } else {
           out.medium_refs.push_back(emit_prim(n, xf, nullptr, nullptr));
         }
@@ -571,6 +575,8 @@ int flatten_scene(const Tree& t, int world, int lights, HostScene& out) {
   Flattener f(t, out);
   const char* bl = getenv("RT_BOX_LEAVES");
   f.box_leaves_on = !(bl && *bl && atoi(bl) == 0);
+  const char* bsr = getenv("RT_BIG_SPHERE_R");  // A/B: a huge value keeps every sphere in the BVH
+  f.big_r = bsr && *bsr ? atof(bsr) : kBigSphereR;
   int rc = f.walk(world, Xf{}, 1, 0);
   if (timing)
     fprintf(stderr, "[rt] flatten walk %.3f s\n",

@@ -58,6 +58,7 @@ uint32_t scene_features(const HostScene& h, bool* noise_table0) {
     prim(r);
   }
   for (uint32_t r : h.medium_refs) prim(r);
+  for (uint32_t r : h.big_refs) prim(r);
   for (const DevLight& l : h.lights) prim(l.ref);
   if (!h.media.empty()) f |= FT_MEDIA;
   for (const DevMedium& m : h.media) use_mat(m.phase_mat);

@@ -162,6 +162,7 @@ struct DevScene {
   const F4* leafprims;  // 4 x F4 per leaf entry, parallel to refs (see "leaf records")
   const F4* nodes8;     // BVH8 (host_bvh8.cpp layout), root = node 0; null when not built
   const F4* recs8;      // the BVH8's leaf records (leaf record format), in node order
+  const F4* big_recs;   // n_big sphere leaf records: radius >= kBigSphereR, not in the BVH
   uint32_t root;
   int32_t n_nodes;
   const DevMedium* media;
@@ -196,7 +197,7 @@ struct DevScene {
   int32_t shade_lds;    // record-loop kernel of the lean set: F4 offset of the quads' shade
                         // table in the dynamic LDS (after the record pairs), or -1
   int32_t shade_n;      // F4s of that table (2 per quad: normal | kind, solid colour)
-  int32_t _pad_sc2;
+  int32_t n_big;        // world spheres tested before the BVH (big_recs, fp64)
 };
 
 }  // namespace rt

@@ -37,6 +37,11 @@ RT_D void finish_hit(const Params& P, const Path& s, Hit& best) {
   if (HAS(FT_TRI) && best.ref != PRIM_NONE && (best.ref >> 30) == PRIM_TRI)
     refine_tri_hit(P.sc, best.ref & 0x3FFFFFFFu, s.o, s.d, best.t, best.u, best.v);
 #endif
+#ifdef RT_SPHERE32_LEAVES
+  // a BVH sphere leaf won (fp32 test): its t in fp64 (v = -1: a big sphere, fp64 already)
+  if (HAS(FT_SPHERE) && best.ref != PRIM_NONE && (best.ref >> 30) == PRIM_SPHERE && best.v >= 0.0f)
+    refine_sphere_hit(P.sc, best.ref & 0x3FFFFFFFu, s.o, s.d, s.time, best.t);
+#endif
 #ifdef ABL_NO_MEDIA
   if (false)
 #else
@@ -168,7 +173,7 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
     const uint32_t c = grab_chunk(P, b, !has);
     if (c != 0xFFFFFFFFu) {
       start_sample<false, cam_mode(FT)>(P, slot, s, c, 0);
-      trav_init(P.sc, s.d, tr);
+      trav_init<FT>(P.sc, s.o, s.d, s.time, tr);
       has = true;
     }
     PH_ADD(PH_GRAB, t_grab);
@@ -218,7 +223,7 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
 #endif
         PH_T(t_shade);
         if (shade_core<false, FT>(P, slot, s, best, ws, sa) == OUT_NEED_CHUNK) has = false;
-        else trav_init(P.sc, s.d, tr);
+        else trav_init<FT>(P.sc, s.o, s.d, s.time, tr);
         PH_ADD(PH_SHADE, t_shade);
       }
     }

@@ -40,6 +40,9 @@ struct Tree {
 };
 
 // Host copy of the flattened scene plus its device mirror.
+// World spheres this large stay out of the BVH and are tested in fp64 at the start of every
+// ray (trav_init): the BVH's sphere leaves are then all small and tested in fp32
+constexpr double kBigSphereR = 256.0;
 struct HostScene {
   std::vector<F4> sph_cr, sph_mv;
   std::vector<F2> sph_uv;
@@ -57,6 +60,8 @@ struct HostScene {
   std::vector<float> prim_bounds;  // 6 per world ref (export/tests)
   std::vector<DevMedium> media;
   std::vector<uint32_t> medium_refs;
+  std::vector<uint32_t> big_refs;  // world spheres of radius >= kBigSphereR: tested in fp64
+                                   // by every ray before the BVH (not BVH prims)
   int32_t medium_draws = 0;
   std::vector<DevLight> lights;
   std::vector<DevMaterial> mats;

@@ -247,25 +247,9 @@ RT_D bool hit_prim(const DevScene& sc, uint32_t ref, f3 o, f3 d, float time, flo
 }
 
 // ---- leaf-record tests (traversal; same semantics as the per-type tests) ----
-RT_D bool hit_sphere_rec(const F4 r[4], f3 o, f3 d, float time, float tmin, float tmax,
-                         float& t_out) {
+RT_D bool hit_sphere_rec64(const F4 r[4], f3 o, f3 d, float time, float tmin, float tmax,
+                           float& t_out) {
   const F4 c0 = r[0], mv = r[1];
-#ifdef RT_ABLATE_SPHERE32  // timing ablation only (the naive fp32 quadratic; not the product)
-  {
-    const f3 oc = mk3(c0.x + time * mv.x, c0.y + time * mv.y, c0.z + time * mv.z) - o;
-    const float a = dot(d, d), h = dot(d, oc), cc = dot(oc, oc) - mv.w * mv.w;
-    const float disc = h * h - a * cc;
-    if (disc < 0.0f) return false;
-    const float sq = fsqrt(disc), ia = rcp(a);
-    float root = (h - sq) * ia;
-    if (!(tmin < root && root < tmax)) {
-      root = (h + sq) * ia;
-      if (!(tmin < root && root < tmax)) return false;
-    }
-    t_out = root;
-    return true;
-  }
-#endif
   double cx = (double)c0.x + (double)time * (double)mv.x;
   double cy = (double)c0.y + (double)time * (double)mv.y;
   double cz = (double)c0.z + (double)time * (double)mv.z;
@@ -290,6 +274,57 @@ RT_D bool hit_sphere_rec(const F4 r[4], f3 o, f3 d, float time, float tmin, floa
   }
   t_out = (float)(q * __builtin_amdgcn_rcp(a));  // fp32-level result from fp64 q: float t
   return true;
+}
+// Measured slower, kept opt-in (-DRT_SPHERE32_LEAVES; C3 +3.6 %, C4 +5.4 %, C5 +3.8 % against
+// the fp64 leaves, profiles/r4_sphere_leaves_ab.jsonl): the BVH's sphere leaves (radius
+// < kBigSphereR) in fp32 with the numerically robust discriminant r^2 - |oc - (h/a) d|^2
+// (no cancellation of |oc|^2 against r^2), falling back to the fp64 test where the fp32
+// result is uncertain: the discriminant within its rounding bound (a grazing ray) or a
+// root next to tmin or tmax (a self-hit or a near-tie with the closest hit so far).  The
+// winner's t is re-solved in fp64 once per segment (refine_sphere_hit).
+RT_D bool hit_sphere_rec32(const F4 r[4], f3 o, f3 d, float time, float tmin, float tmax,
+                           float& t_out) {
+  const F4 c0 = r[0], mv = r[1];
+  const f3 oc = mk3(fmaf(time, mv.x, c0.x), fmaf(time, mv.y, c0.y), fmaf(time, mv.z, c0.z)) - o;
+  const float a = dot(d, d), ia = rcp(a), h = dot(d, oc);
+  const float s = h * ia;  // the ray's closest approach to the center
+  const f3 f = mk3(fmaf(-s, d.x, oc.x), fmaf(-s, d.y, oc.y), fmaf(-s, d.z, oc.z));
+  const float ff = dot(f, f), rr = mv.w * mv.w, q = rr - ff;  // disc / a
+  // rounding of f ~ eps |oc| per component: |ff| off by ~4 eps |f| |oc|
+  const float err = 6.0e-7f * (rr + fsqrt(ff * dot(oc, oc)));
+  if (fabsf(q) <= err) return hit_sphere_rec64(r, o, d, time, tmin, tmax, t_out);
+  if (q < 0.0f) return false;
+  const float sq = fsqrt(q * ia);  // sqrt(disc) / a
+  float root = s - sq;
+  const float tol = 1.0e-5f * (fabsf(root) + tmin);
+  if (fabsf(root - tmin) <= tol || fabsf(root - tmax) <= 1.0e-5f * fabsf(root))
+    return hit_sphere_rec64(r, o, d, time, tmin, tmax, t_out);
+  if (!(tmin < root && root < tmax)) {
+    root = s + sq;
+    if (fabsf(root - tmin) <= 1.0e-5f * (fabsf(root) + tmin) ||
+        fabsf(root - tmax) <= 1.0e-5f * fabsf(root))
+      return hit_sphere_rec64(r, o, d, time, tmin, tmax, t_out);
+    if (!(tmin < root && root < tmax)) return false;
+  }
+  t_out = root;
+  return true;
+}
+RT_D bool hit_sphere_rec(const F4 r[4], f3 o, f3 d, float time, float tmin, float tmax,
+                         float& t_out) {
+#ifdef RT_SPHERE32_LEAVES
+  return hit_sphere_rec32(r, o, d, time, tmin, tmax, t_out);
+#else
+  return hit_sphere_rec64(r, o, d, time, tmin, tmax, t_out);
+#endif
+}
+// The winning sphere's t re-solved in fp64 (hit_sphere_d's quadratic on the same fp32
+// ray): the root nearest to the fp32 test's, so the refinement never changes which root
+// (entering or leaving) the traversal chose
+RT_D void refine_sphere_hit(const DevScene& sc, uint32_t idx, f3 o, f3 d, float time, float& t_io) {
+  double r0, r1;
+  if (!sphere_roots_d(sc, idx, o, d, time, r0, r1)) return;  // fp32 hit, fp64 grazing miss
+  const double t = (double)t_io;
+  t_io = (float)(fabs(r0 - t) <= fabs(r1 - t) ? r0 : r1);
 }
 RT_D bool hit_quad_rec(const F4 r[4], f3 o, f3 d, float tmin, float tmax, float& t_out,
                        float& a_out, float& b_out) {

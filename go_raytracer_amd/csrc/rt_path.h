@@ -48,6 +48,7 @@ struct Params {
   DevScene sc;
   FastDiv fd_width, fd_s;
   FastDiv fd_gchunks, fd_gpix;  // chunk order: groups of fd_gpix.d pixels x all sample blocks
+  FastDiv fd_gchunks2;          // the tail phase's chunks per group (gpix x its blocks)
   // camera (initialize camera.go:179-253, converted to fp32)
   float p00r[3], du[3], dv[3], cc[3], dku[3], dkv[3];  // p00r = pixel00 - center
   float bg[3];
@@ -55,7 +56,10 @@ struct Params {
   int s, defocus, max_depth;
   int width, rank, nranks;
   uint32_t npix;       // pixels of this rank
-  uint32_t K;          // samples per chunk
+  uint32_t K;          // samples per chunk (first phase)
+  uint32_t K2;         // samples per chunk of the tail phase (chunk ids >= n1)
+  uint32_t S1;         // samples [0, S1) of every pixel in the first phase, [S1, ss) in the tail
+  uint32_t n1;         // chunks of the first phase (npix * S1 / K)
   uint32_t n_chunks;
   uint32_t P;          // path slots (stack column count)
   uint32_t ss;         // s*s
@@ -179,9 +183,33 @@ RT_D uint32_t wave_uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v
 struct Ids {
   uint32_t lpix, gpix, row, col, sample0, count;
 };
+typedef __attribute__((address_space(4))) const Params cst_params;
+// The launch parameters re-read through the scalar cache where they are used: the asm
+// barrier hides that the pointer is the kernel-argument segment's, so the compiler
+// cannot hoist the loads to the kernel entry and hold the values in SGPRs across the
+// whole loop (where they spill to VGPR lanes).
+RT_D const cst_params* kparams() {
+  const cst_params* p = (const cst_params*)__builtin_amdgcn_kernarg_segment_ptr();
+  __asm__ volatile("" : "+s"(p));
+  return p;
+}
+// Two phases (render_impl): chunk ids [0, n1) cover samples [0, S1) of every pixel in
+// chunks of K, ids [n1, n_chunks) the rest in chunks of K2 <= K, both in row-group order.
+// The partitioned grab hands out the first phase before the tail, so the render's last
+// chunks are short (the tail that idles lanes) while most samples pay the per-chunk cost of
+// the large K.  `sub` is the sample block in its phase's units.
+// (the tail's parameters are read from the kernel-argument segment where used, kparams:
+// held in SGPRs for the whole kernel they cost the mesh and book1 kernels ~45 SGPR spills)
 RT_D uint32_t chunk_pixel(const Params& P, uint32_t chunk, uint32_t& sub) {
-  const uint32_t q = fdiv(chunk, P.fd_gchunks);
-  const uint32_t r = chunk - q * P.fd_gchunks.d;
+  const cst_params* kp = kparams();
+  const uint32_t n1 = kp->n1;
+  const bool tail = chunk >= n1;
+  const uint32_t c = tail ? chunk - n1 : chunk;
+  const FastDiv fg = tail ? FastDiv{kp->fd_gchunks2.m, kp->fd_gchunks2.s1, kp->fd_gchunks2.s2,
+                                    kp->fd_gchunks2.d}
+                          : P.fd_gchunks;
+  const uint32_t q = fdiv(c, fg);
+  const uint32_t r = c - q * fg.d;
   sub = fdiv(r, P.fd_gpix);
   return q * P.fd_gpix.d + (r - sub * P.fd_gpix.d);
 }
@@ -193,9 +221,18 @@ RT_D Ids chunk_ids(const Params& P, uint32_t chunk) {
   r.col = r.lpix - row_l * (uint32_t)P.width;
   r.row = row_l * (uint32_t)P.nranks + (uint32_t)P.rank;
   r.gpix = r.row * (uint32_t)P.width + r.col;
-  r.sample0 = sub * P.K;
-  r.count = min(P.K, P.ss - r.sample0);
+  const cst_params* kp = kparams();
+  const bool tail = chunk >= kp->n1;
+  const uint32_t S1 = kp->S1, K2 = kp->K2;
+  r.sample0 = tail ? S1 + sub * K2 : sub * P.K;
+  r.count = tail ? min(K2, P.ss - r.sample0) : min(P.K, S1 - r.sample0);
   return r;
+}
+// samples in the chunk whose first sample is s0 (chunk_ids().count)
+RT_D uint32_t chunk_count(const Params& P, uint32_t s0) {
+  const cst_params* kp = kparams();
+  const uint32_t S1 = kp->S1;
+  return s0 < S1 ? min(P.K, S1 - s0) : min(kp->K2, P.ss - s0);
 }
 
 // The camera constants in LDS (every kernel that starts samples stages them once,
@@ -225,16 +262,6 @@ constexpr int cam_mode(uint32_t ft) {
 #else
   return ft == FT_SET_BOOK2 ? 1 : 2;
 #endif
-}
-typedef __attribute__((address_space(4))) const Params cst_params;
-// The launch parameters re-read through the scalar cache where they are used: the asm
-// barrier hides that the pointer is the kernel-argument segment's, so the compiler
-// cannot hoist the loads to the kernel entry and hold the values in SGPRs across the
-// whole loop (where they spill to VGPR lanes).
-RT_D const cst_params* kparams() {
-  const cst_params* p = (const cst_params*)__builtin_amdgcn_kernarg_segment_ptr();
-  __asm__ volatile("" : "+s"(p));
-  return p;
 }
 RT_D void stage_camera(const Params& P) {  // before a __syncthreads of every thread
   if (threadIdx.x == 0) {
@@ -373,12 +400,26 @@ struct Trav {
                  // subtree is traversed), taking the LDS latency off the pop
   Hit best;
 };
-RT_D void trav_init(const DevScene& sc, f3 d, Trav& tr) {
+// A new ray: the traversal state, and the spheres kept out of the BVH (radius >=
+// kBigSphereR: the ground spheres of book1 and the mesh scene) tested first, in fp64, by
+// every lane at once (a uniform loop over scalar-loaded records), so the BVH's sphere
+// leaves are all small and tested in fp32 (hit_sphere_rec32) without a divergent fp64
+// branch.  Their hit's v = -1 tells finish_hit that t is already fp64-solved.
+template <uint32_t FT>
+RT_D void trav_init(const DevScene& sc, f3 o, f3 d, float time, Trav& tr) {
   tr.inv = mk3(rcp(d.x), rcp(d.y), rcp(d.z));
   tr.cur = sc.root == PRIM_NONE ? TRAV_DONE : sc.root;
   tr.sp = 0;
   tr.top = 0;
   tr.best = {kInf, 0.0f, 0.0f, PRIM_NONE};
+  if (HAS(FT_SPHERE))
+    for (int i = 0; i < sc.n_big; ++i) {
+      const F4* q = sc.big_recs + 4 * (size_t)__builtin_amdgcn_readfirstlane(i);
+      const F4 rec[4] = {ld_cst(q), ld_cst(q + 1), ld_cst(q + 2), ld_cst(q + 3)};
+      float t;
+      if (hit_sphere_rec64(rec, o, d, time, 0.001f, tr.best.t, t))
+        tr.best = {t, 0.0f, -1.0f, fbits(rec[0].w)};
+    }
 }
 
 // LDS instantiation: lnodes holds the node array and, when recs_lds, the leaf
@@ -1025,7 +1066,7 @@ template <bool LDS, uint32_t FT>
 RT_D void trace_world(const DevScene& sc, const F4* lnodes, bool recs_lds, const TravStack& stack,
                       f3 o, f3 d, float time, float tmin, Hit& best) {
   Trav tr;
-  trav_init(sc, d, tr);
+  trav_init<FT>(sc, o, d, time, tr);
   trav_steps<LDS, FT>(sc, lnodes, recs_lds, stack, o, d, time, tmin, tr, 0x7FFFFFFF);
   best = tr.best;
 }
@@ -1923,7 +1964,7 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
   if (isnan(L.x) || isnan(L.y) || isnan(L.z)) printf("NAN gpix %u sample %u\n", s.gpix, s.s0 + s.j);
 #endif
   sa.add(P, s.chunk, L);
-  const uint32_t count = min(P.K, P.ss - s.s0);  // chunk_ids().count
+  const uint32_t count = chunk_count(P, s.s0);
   if (s.j + 1 < count) {
     if (!have_rcam)  // a miss, or the depth limit: the camera draw is made here
       rcam = rt_rng_draw(P.seed, s.gpix, s.s0 + s.j + 1, RT_STREAM_CAMERA);

@@ -155,12 +155,15 @@ __global__ __launch_bounds__(256) void k_resolve(Params P, float* out, double sc
   unsigned long long cs[3] = {0ull, 0ull, 0ull};
   if (P.csum) {
     const uint32_t gpix = P.fd_gpix.d, q = fdiv(lp, P.fd_gpix), r = lp - q * gpix;
-    const uint32_t cpp = P.fd_gchunks.d / gpix;
-    const unsigned long long* rec = P.csum + 4 * ((size_t)q * P.fd_gchunks.d + r);
-    for (uint32_t sb = 0; sb < cpp; ++sb, rec += 4 * (size_t)gpix) {
-      cs[0] += rec[0];
-      cs[1] += rec[1];
-      cs[2] += rec[2];
+    for (int ph = 0; ph < 2; ++ph) {  // the first phase's chunks, then the tail's
+      const uint32_t gch = ph ? P.fd_gchunks2.d : P.fd_gchunks.d;
+      const uint32_t cpp = gch / gpix;
+      const unsigned long long* rec = P.csum + 4 * ((ph ? (size_t)P.n1 : 0) + (size_t)q * gch + r);
+      for (uint32_t sb = 0; sb < cpp; ++sb, rec += 4 * (size_t)gpix) {
+        cs[0] += rec[0];
+        cs[1] += rec[1];
+        cs[2] += rec[2];
+      }
     }
   }
   for (int ch = 0; ch < 3; ++ch) {
@@ -736,6 +739,12 @@ static int upload_scene(const Scene* s, DeviceScene* ds) {
 records_done:
   UP(h.media, media);
   UP(h.medium_refs, medium_refs);
+  {  // spheres tested before the BVH (host_flatten: radius >= kBigSphereR), as leaf records
+    std::vector<F4> br(4 * h.big_refs.size());
+    for (size_t i = 0; i < h.big_refs.size(); ++i) make_record(h, h.big_refs[i], &br[4 * i]);
+    UP(br, big_recs);
+    d.n_big = (int32_t)h.big_refs.size();
+  }
   UP(h.lights, lights);
   UP(mats, mats);
   UP(h.texs, texs);
@@ -985,7 +994,8 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   if (o.chunk > 0) {
     K = (uint32_t)o.chunk;
   } else if (mode == RT_MODE_FUSED) {
-    const uint64_t work = (uint64_t)npix * ss, need = (uint64_t)(f_lds ? 12u : 100u) * P;
+    const uint64_t work = (uint64_t)npix * ss,
+                   need = (uint64_t)std::max(1, env_int("RT_CHUNK_NEED", f_lds ? 12 : 100)) * P;
     K = f_lds ? 8u : 4u;  // the smallest: C3's 8-GPU share 6 % faster at 4 than 8 (C2's ±1 %)
     for (uint32_t k : {32u, 16u, 8u})
       if (work / k >= need) {
@@ -994,7 +1004,26 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
       }
   }
   K = std::max<uint32_t>(1u, std::min<uint32_t>(std::min(K, ss), 4096u));
-  const uint32_t cpp = (ss + K - 1) / K;
+  // Tail phase (fused, default chunk sizes): the last ~1/RT_TAIL_FRAC of every pixel's
+  // samples in chunks of K / 4 (min 4), after all first-phase chunks (rt_path.h chunk_pixel),
+  // by default (1/4) when a lane gets fewer than 40 chunks: the multi-GPU shares.  C2's 2-,
+  // 4- and 8-GPU shares -1.0 / -4.0 / -2.3 %, the whole image (52 chunks per lane, no tail)
+  // +0.5 % with it (profiles/r4_tail_ab.jsonl)
+  uint32_t S1 = ss, K2 = K;
+  {
+    const bool few = mode == RT_MODE_FUSED &&
+                     (uint64_t)npix * ss / std::max<uint32_t>(K, 1u) < 40ull * P;
+    const int tf = env_int("RT_TAIL_FRAC", few ? 4 : 0);
+    if (mode == RT_MODE_FUSED && o.chunk <= 0 && tf > 1 && K >= 8u) {
+      K2 = std::max<uint32_t>(4u, (uint32_t)env_int("RT_TAIL_K", (int)(K / 4)));
+      const uint32_t s1 = (uint32_t)((uint64_t)ss * (uint32_t)(tf - 1) / (uint32_t)tf) / K * K;
+      if (s1 > 0 && s1 < ss && K2 < K) S1 = s1;
+      else K2 = K;
+    }
+  }
+  const uint32_t cpp1 = S1 / K + (S1 == ss && ss % K ? 1u : 0u);  // no tail: ceil(ss / K)
+  const uint32_t cpp2 = S1 < ss ? (ss - S1 + K2 - 1) / K2 : 0u;
+  const uint32_t cpp = cpp1 + cpp2;
   const uint64_t n_chunks64 = (uint64_t)npix * cpp;
   if (n_chunks64 >= 0xF0000000ull) return set_error(RT_ERR_UNSUPPORTED, "too many work chunks");
   const uint32_t n_chunks = (uint32_t)n_chunks64;
@@ -1080,6 +1109,9 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   p.nranks = o.nranks;
   p.npix = npix;
   p.K = K;
+  p.K2 = K2;
+  p.S1 = S1;
+  p.n1 = npix * cpp1;
   p.n_chunks = n_chunks;
   p.P = P;
   p.ss = ss;
@@ -1094,7 +1126,8 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     while (rows % grows) --grows;  // a divisor of the rank's row count
     const uint32_t gpix = std::max<uint32_t>(1u, grows * W);
     p.fd_gpix = make_fastdiv(gpix);
-    p.fd_gchunks = make_fastdiv(gpix * cpp);
+    p.fd_gchunks = make_fastdiv(gpix * cpp1);
+    p.fd_gchunks2 = make_fastdiv(std::max<uint32_t>(1u, gpix * cpp2));
   }
   p.fd_width = make_fastdiv(W);
   p.fd_s = make_fastdiv((uint32_t)cd.spp_sqrt);
