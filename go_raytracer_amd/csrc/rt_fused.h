@@ -172,7 +172,7 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
     PH_T(t_grab);
     const uint32_t c = grab_chunk(P, b, !has);
     if (c != 0xFFFFFFFFu) {
-      start_sample<false, cam_mode(FT)>(P, slot, s, c, 0);
+      start_sample<false, cam_mode(FT), FT == 0u && TREE == 0>(P, slot, s, c, 0);
       trav_init<FT>(P.sc, s.o, s.d, s.time, tr);
       has = true;
     }

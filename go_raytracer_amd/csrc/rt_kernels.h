@@ -133,10 +133,13 @@ RT_D bool hit_sphere_d(const DevScene& sc, uint32_t i, f3 o, f3 d, float time, d
 }
 // Both roots of the sphere quadratic, as hit_sphere_d computes them (same
 // arithmetic, so identical doubles): r0 <= r1.  False when the ray misses.
+RT_D bool sphere_roots_cm(F4 cr, F4 mv, f3 o, f3 d, float time, double& r0, double& r1);
 RT_D bool sphere_roots_d(const DevScene& sc, uint32_t i, f3 o, f3 d, float time, double& r0,
                          double& r1) {
-  const F4 cr = sc.sph_cr[i];
-  const F4 mv = sc.sph_mv[i];
+  return sphere_roots_cm(sc.sph_cr[i], sc.sph_mv[i], o, d, time, r0, r1);
+}
+// the same from the sphere's center | radius and motion records
+RT_D bool sphere_roots_cm(F4 cr, F4 mv, f3 o, f3 d, float time, double& r0, double& r1) {
   double cx = (double)cr.x + (double)time * (double)mv.x;
   double cy = (double)cr.y + (double)time * (double)mv.y;
   double cz = (double)cr.z + (double)time * (double)mv.z;

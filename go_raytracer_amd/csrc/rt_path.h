@@ -21,6 +21,9 @@ constexpr int kMaxParts = 64;    // chunk-range partitions of the fused kernel (
 constexpr int kPartStride = 64;  // u32 between partition counters (256 B: own cache lines)
 
 enum : uint32_t { F_PEND = 1u, F_PRE = 2u, F_NONFINITE = 4u };
+// Path::flags above this bit: the sample count of the path's chunk (chunk_ids().count, set
+// when the chunk starts), so the per-sample "last sample?" test needs no launch parameter
+constexpr uint32_t kCountShift = 8;
 enum { OUT_DEAD = 0, OUT_ALIVE = 1, OUT_NEED_CHUNK = 2 };
 
 struct Counters {
@@ -213,9 +216,26 @@ RT_D uint32_t chunk_pixel(const Params& P, uint32_t chunk, uint32_t& sub) {
   sub = fdiv(r, P.fd_gpix);
   return q * P.fd_gpix.d + (r - sub * P.fd_gpix.d);
 }
+// ONE: a launch without a tail phase (S1 = ss), with the launch parameters held in SGPRs:
+// the record-loop kernel, whose chunk starts lost 3 % to the tail mapping's kernel-argument
+// loads (profiles/r4_tail_code_ab.jsonl); render_impl never gives it a tail
+template <bool ONE = false>
 RT_D Ids chunk_ids(const Params& P, uint32_t chunk) {
   Ids r;
   uint32_t sub;
+  if (ONE) {
+    const uint32_t q = fdiv(chunk, P.fd_gchunks);
+    const uint32_t rr = chunk - q * P.fd_gchunks.d;
+    sub = fdiv(rr, P.fd_gpix);
+    r.lpix = q * P.fd_gpix.d + (rr - sub * P.fd_gpix.d);
+    const uint32_t row_l = fdiv(r.lpix, P.fd_width);
+    r.col = r.lpix - row_l * (uint32_t)P.width;
+    r.row = row_l * (uint32_t)P.nranks + (uint32_t)P.rank;
+    r.gpix = r.row * (uint32_t)P.width + r.col;
+    r.sample0 = sub * P.K;
+    r.count = min(P.K, P.ss - r.sample0);
+    return r;
+  }
   r.lpix = chunk_pixel(P, chunk, sub);
   uint32_t row_l = fdiv(r.lpix, P.fd_width);
   r.col = r.lpix - row_l * (uint32_t)P.width;
@@ -227,12 +247,6 @@ RT_D Ids chunk_ids(const Params& P, uint32_t chunk) {
   r.sample0 = tail ? S1 + sub * K2 : sub * P.K;
   r.count = tail ? min(K2, P.ss - r.sample0) : min(P.K, S1 - r.sample0);
   return r;
-}
-// samples in the chunk whose first sample is s0 (chunk_ids().count)
-RT_D uint32_t chunk_count(const Params& P, uint32_t s0) {
-  const cst_params* kp = kparams();
-  const uint32_t S1 = kp->S1;
-  return s0 < S1 ? min(P.K, S1 - s0) : min(kp->K2, P.ss - s0);
 }
 
 // The camera constants in LDS (every kernel that starts samples stages them once,
@@ -1100,7 +1114,18 @@ RT_D void trace_media(const Params& P, f3 o, f3 d, float time, float tmin, uint3
   int cached_group = -1;
   const float ray_len = length(d);
   for (int mi = 0; mi < sc.n_media; ++mi) {
-    const DevMedium m = sc.media[mi];
+    // the medium record and its boundary through the scalar cache (a uniform index: no
+    // vector-memory load, and no s_waitcnt vmcnt on the traversal's outstanding loads)
+    static_assert(sizeof(DevMedium) == 32, "DevMedium: two 16-B scalar loads");
+    const F4* mr = (const F4*)(sc.media + __builtin_amdgcn_readfirstlane(mi));
+    const F4 ma = ld_cst(mr), mb = ld_cst(mr + 1);
+    DevMedium m;
+    m.bfirst = fbits(ma.x);
+    m.bcount = fbits(ma.y);
+    m.neg_inv_density = ma.z;
+    m.phase_mat = (int32_t)fbits(ma.w);
+    m.draw_base = (int32_t)fbits(mb.x);
+    m.mult = (int32_t)fbits(mb.y);
     // The free-flight distance first (its draws are a pure function of the path's
     // counters, rt_rng.h, so drawing them before the boundary test changes nothing).
     // The medium's hit lies at max(t1, tmin) + hd / |d| > hd / |d|: when that is already
@@ -1128,13 +1153,16 @@ RT_D void trace_media(const Params& P, f3 o, f3 d, float time, float tmin, uint3
     if (!(hd_t < best.t)) continue;
 #endif
     double t1, t2;
-    const uint32_t b0 = m.bcount == 1 ? sc.medium_refs[m.bfirst] : PRIM_NONE;
+    typedef __attribute__((address_space(4))) const uint32_t cst_u32;
+    const uint32_t b0 = m.bcount == 1 ? *(const cst_u32*)(sc.medium_refs + m.bfirst) : PRIM_NONE;
     if ((b0 >> 30) == PRIM_SPHERE && b0 != PRIM_NONE) {
       // a sphere boundary (book2's fog and glass-ball interior): one quadratic gives
       // both boundary.Hit calls of medium.go:33-42 — t1 = the smaller root (always
       // inside (-inf, inf)), t2 = the larger one if it exceeds t1 + 1e-4
       double r0, r1;
-      if (!sphere_roots_d(sc, b0 & 0x3FFFFFFFu, o, d, time, r0, r1)) continue;
+      const uint32_t bi = b0 & 0x3FFFFFFFu;
+      if (!sphere_roots_cm(ld_cst(sc.sph_cr + bi), ld_cst(sc.sph_mv + bi), o, d, time, r0, r1))
+        continue;
       t1 = r0;
       if (!(t1 + 0.0001 < r1 && r1 < (double)kInf)) continue;
       t2 = r1;
@@ -1650,7 +1678,7 @@ RT_D void load_path(const Params& P, uint32_t slot, Path& s) {
   s.j = ps.y & 0xFFFu;
   s.k = (ps.y >> 12) & 0xFFu;
   s.nst = (ps.y >> 20) & 0xFFu;
-  s.flags = ps.y >> 28;
+  s.flags = (ps.y >> 28) | (id.count << kCountShift);
 }
 
 // the next sample of the same chunk, its camera draw already made: the path
@@ -1666,14 +1694,14 @@ RT_D void next_sample(const Params& P, uint32_t slot, Path& s, uint32_t j, const
   s.j = j;
   s.k = 0;
   s.nst = 0;
-  s.flags = 0;
+  s.flags &= ~((1u << kCountShift) - 1u);  // the chunk's sample count stays
   store_ray<SOA>(P, slot, s);
 }
 
 // camera ray for sample j of `chunk` (path state reset)
-template <bool SOA, int CAM = 0>
+template <bool SOA, int CAM = 0, bool ONE = false>
 RT_D void start_sample(const Params& P, uint32_t slot, Path& s, uint32_t chunk, uint32_t j) {
-  Ids id = chunk_ids(P, chunk);
+  Ids id = chunk_ids<ONE>(P, chunk);
   const rt_u32x4 r = rt_rng_draw(P.seed, id.gpix, id.sample0 + j, RT_STREAM_CAMERA);
   camera_ray_r<CAM>(P, id, id.sample0 + j, r, s.o, s.d, s.time);
   s.spare = rt_spare24(r);
@@ -1683,7 +1711,7 @@ RT_D void start_sample(const Params& P, uint32_t slot, Path& s, uint32_t chunk, 
   s.j = j;
   s.k = 0;
   s.nst = 0;
-  s.flags = 0;
+  s.flags = id.count << kCountShift;
   store_ray<SOA>(P, slot, s);
 }
 
@@ -1964,7 +1992,7 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
   if (isnan(L.x) || isnan(L.y) || isnan(L.z)) printf("NAN gpix %u sample %u\n", s.gpix, s.s0 + s.j);
 #endif
   sa.add(P, s.chunk, L);
-  const uint32_t count = chunk_count(P, s.s0);
+  const uint32_t count = s.flags >> kCountShift;  // chunk_ids().count
   if (s.j + 1 < count) {
     if (!have_rcam)  // a miss, or the depth limit: the camera draw is made here
       rcam = rt_rng_draw(P.seed, s.gpix, s.s0 + s.j + 1, RT_STREAM_CAMERA);

@@ -155,9 +155,9 @@ __global__ __launch_bounds__(256) void k_resolve(Params P, float* out, double sc
   unsigned long long cs[3] = {0ull, 0ull, 0ull};
   if (P.csum) {
     const uint32_t gpix = P.fd_gpix.d, q = fdiv(lp, P.fd_gpix), r = lp - q * gpix;
-    for (int ph = 0; ph < 2; ++ph) {  // the first phase's chunks, then the tail's
+    for (int ph = 0; ph < 2; ++ph) {  // the first phase's chunks, then the tail's (if any)
       const uint32_t gch = ph ? P.fd_gchunks2.d : P.fd_gchunks.d;
-      const uint32_t cpp = gch / gpix;
+      const uint32_t cpp = ph && P.S1 >= P.ss ? 0u : gch / gpix;
       const unsigned long long* rec = P.csum + 4 * ((ph ? (size_t)P.n1 : 0) + (size_t)q * gch + r);
       for (uint32_t sb = 0; sb < cpp; ++sb, rec += 4 * (size_t)gpix) {
         cs[0] += rec[0];
@@ -1011,11 +1011,16 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   // +0.5 % with it (profiles/r4_tail_ab.jsonl)
   uint32_t S1 = ss, K2 = K;
   {
-    const bool few = mode == RT_MODE_FUSED &&
+    // (not the record-loop kernel: its chunk starts use the one-phase mapping, chunk_ids<true>)
+    const bool one_phase = tree == 0 && ft_set == 0u;
+    const bool few = mode == RT_MODE_FUSED && !one_phase &&
                      (uint64_t)npix * ss / std::max<uint32_t>(K, 1u) < 40ull * P;
-    const int tf = env_int("RT_TAIL_FRAC", few ? 4 : 0);
-    if (mode == RT_MODE_FUSED && o.chunk <= 0 && tf > 1 && K >= 8u) {
-      K2 = std::max<uint32_t>(4u, (uint32_t)env_int("RT_TAIL_K", (int)(K / 4)));
+    // default: with the default chunk size only; an explicit RT_TAIL_FRAC also applies to
+    // an explicit chunk size (A/B and tests)
+    const int tf_env = env_int("RT_TAIL_FRAC", -1);
+    const int tf = tf_env >= 0 ? tf_env : (few && o.chunk <= 0 ? 4 : 0);
+    if (mode == RT_MODE_FUSED && !one_phase && tf > 1 && K >= 8u) {
+      K2 = std::max<uint32_t>(1u, (uint32_t)env_int("RT_TAIL_K", (int)std::max<uint32_t>(4u, K / 4)));
       const uint32_t s1 = (uint32_t)((uint64_t)ss * (uint32_t)(tf - 1) / (uint32_t)tf) / K * K;
       if (s1 > 0 && s1 < ss && K2 < K) S1 = s1;
       else K2 = K;

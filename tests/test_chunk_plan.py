@@ -1,5 +1,5 @@
 """CPU model of the fused kernel's chunk plan (rt_render.hip render_impl, rt_path.h
-chunk_pixel / chunk_ids / chunk_count, rt_render.hip k_resolve): every sample of every
+chunk_pixel / chunk_ids, rt_render.hip k_resolve): every sample of every
 pixel belongs to exactly one chunk, the chunks k_resolve sums for a pixel are exactly the
 chunks whose ids map to it, and the two-phase plan (a first phase of K-sample chunks, then a
 tail of K2-sample chunks) changes only how samples are grouped.  Pixel sums are exact integer
@@ -39,19 +39,13 @@ def chunk_ids(p, c):
     return lp, s0, cnt
 
 
-def chunk_count(p, s0):
-    return min(p["K"], p["S1"] - s0) if s0 < p["S1"] else min(p["K2"], p["ss"] - s0)
-
-
 def resolve_chunks(p, lp):
     """k_resolve: the chunk records it sums for local pixel lp."""
     q, r = divmod(lp, p["gpix"])
     out = []
     for ph in (0, 1):
         gch = p["gch2"] if ph else p["gch"]
-        cpp = gch // p["gpix"]
-        if ph and p["cpp2"] == 0:
-            cpp = 0
+        cpp = 0 if ph and p["S1"] >= p["ss"] else gch // p["gpix"]  # no tail: no second loop
         base = (p["n1"] if ph else 0) + q * gch + r
         out += [base + sb * p["gpix"] for sb in range(cpp)]
     return out
@@ -59,7 +53,7 @@ def resolve_chunks(p, lp):
 
 CASES = [(npix, gpix, ss, K, tf)
          for (npix, gpix), ss, K, tf in itertools.product(
-             [(12, 4), (30, 10), (7, 7)], [1, 9, 16, 484, 1024], [4, 8, 16, 32], [0, 4, 8])]
+             [(12, 4), (30, 10), (7, 7), (5, 1)], [1, 9, 16, 484, 1024], [4, 8, 16, 32], [0, 4, 8])]
 
 
 @pytest.mark.parametrize("npix,gpix,ss,K,tf", CASES)
@@ -71,7 +65,6 @@ def test_every_sample_once_and_resolve_matches(npix, gpix, ss, K, tf):
     for c in range(p["n"]):
         lp, s0, cnt = chunk_ids(p, c)
         assert 0 <= lp < npix and cnt >= 1
-        assert chunk_count(p, s0) == cnt  # shade_core's count from the cached first sample
         for s in range(s0, s0 + cnt):
             seen[lp][s] += 1
         owner.setdefault(lp, []).append(c)

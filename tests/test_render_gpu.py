@@ -48,6 +48,37 @@ def test_bitwise_invariances(rt, gpu, name):
     assert H == cam.derived().height
 
 
+@pytest.mark.parametrize("name", ["book1", "book2", "cornell"])
+def test_tail_phase_is_bitwise(rt, gpu, name, monkeypatch):
+    """The two-phase chunk plan (rt_path.h chunk_pixel: the last samples of every pixel in
+    shorter chunks after all first-phase chunks) regroups samples only; with exact
+    fixed-point pixel sums the image is the same bits for any tail fraction and tail chunk
+    size, and for the one-phase plan (the record-loop kernel ignores the request)."""
+    t, cam, w, l = _scene(rt, name, 48, 64)
+    with rt.Scene(t, w, l) as sc:
+        monkeypatch.setenv("RT_TAIL_FRAC", "0")
+        ref, _ = sc.render(cam, seed=6)
+        for K, tf, tk in ((32, "4", "4"), (32, "8", "3"), (16, "2", "5"), (8, "4", "1")):
+            monkeypatch.setenv("RT_TAIL_FRAC", tf)
+            monkeypatch.setenv("RT_TAIL_K", tk)
+            img, _ = sc.render(cam, seed=6, chunk=K)
+            assert np.array_equal(img, ref, equal_nan=True), (K, tf, tk)
+
+
+def test_big_spheres_outside_the_bvh_same_image(rt, gpu, monkeypatch):
+    """Spheres of radius >= kBigSphereR are tested before the BVH (trav_init) instead of as
+    BVH leaves: the same fp64 test on the same record, so the same closest hits.  book1's
+    ground sphere both ways (RT_BIG_SPHERE_R is read when the scene is created)."""
+    imgs = []
+    for r in ("256", "1e30"):
+        monkeypatch.setenv("RT_BIG_SPHERE_R", r)
+        t, cam, w, l = _scene(rt, "book1", 64, 16)
+        with rt.Scene(t, w, l) as sc:
+            imgs.append(sc.render(cam, seed=8)[0])
+    m = compare(imgs[0], imgs[1])
+    assert m["frac_close"] >= 0.9999 and m["q_equal"] >= 0.9999, m
+
+
 @pytest.mark.parametrize("name,width,spp", [("cornell", 200, 256), ("book2", 96, 256)])
 def test_default_image_independent_of_gpu_count(rt, gpu, name, width, spp):
     """the assembled image of 1, 2 and 8 row shares rendered with
