@@ -131,12 +131,8 @@ constexpr unsigned fused_static_lds(uint32_t ft, int tree = 4) {
   return (unsigned)(fused_short(ft, tree) * 4 + fused_wlds(ft, tree) * 12 + 24) * 256u +
          ((ft & FT_NOISE) ? 256u * 16u + 768u : 0u);
 }
-// TREE: 4 = BVH4, 2 = BVH2, 0 = no tree (every record tested, tiny scenes).
-// TAIL: the record-loop kernel of the lean set maps chunk ids with the one-phase plan
-// (chunk_ids<true>: launch parameters in SGPRs, C2 3 % faster) unless TAIL, its variant
-// for the two-phase plan of small multi-GPU shares (render_impl); the other kernels
-// always take the two-phase mapping.
-template <bool LDS, uint32_t FT, int TREE, bool TAIL = false>
+// TREE: 4 = BVH4, 2 = BVH2, 0 = no tree (every record tested, tiny scenes)
+template <bool LDS, uint32_t FT, int TREE>
 __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) {
   extern __shared__ F4 lnodes[];  // LDS scene cache, sized at launch (scene_lds_bytes)
   __shared__ uint32_t lstack[(fused_short(FT, TREE) > 0 ? fused_short(FT, TREE) : 1) * 256];
@@ -176,7 +172,7 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
     PH_T(t_grab);
     const uint32_t c = grab_chunk(P, b, !has);
     if (c != 0xFFFFFFFFu) {
-      start_sample<false, cam_mode(FT), FT == 0u && TREE == 0 && !TAIL>(P, slot, s, c, 0);
+      start_sample<false, cam_mode(FT), FT == 0u && TREE == 0>(P, slot, s, c, 0);
       trav_init<FT>(P.sc, s.o, s.d, s.time, tr);
       has = true;
     }

@@ -1010,11 +1010,9 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   // 4- and 8-GPU shares -1.0 / -4.0 / -2.3 %, the whole image (52 chunks per lane, no tail)
   // +0.5 % with it (profiles/r4_tail_ab.jsonl)
   uint32_t S1 = ss, K2 = K;
-  // the record-loop kernel of the lean set has a two-phase variant with the records in LDS
-  // only (k_fused's TAIL)
-  const bool rec_loop = tree == 0 && ft_set == kFtSets[0];
   {
-    const bool one_phase = rec_loop && !f_lds;
+    // (not the record-loop kernel: its chunk starts use the one-phase mapping, chunk_ids<true>)
+    const bool one_phase = tree == 0 && ft_set == 0u;
     const bool few = mode == RT_MODE_FUSED && !one_phase &&
                      (uint64_t)npix * ss / std::max<uint32_t>(K, 1u) < 40ull * P;
     // default: with the default chunk size only; an explicit RT_TAIL_FRAC also applies to
@@ -1026,15 +1024,6 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
       const uint32_t s1 = (uint32_t)((uint64_t)ss * (uint32_t)(tf - 1) / (uint32_t)tf) / K * K;
       if (s1 > 0 && s1 < ss && K2 < K) S1 = s1;
       else K2 = K;
-    }
-  }
-  if (rec_loop && S1 < ss) {
-    fused_kernel = (const void*)k_fused<true, kFtSets[0], 0, true>;
-    int tb = 0;  // same launch bounds; launch no more blocks than the variant keeps resident
-    if ((rc = occupancy_blocks(fused_kernel, o.device, &tb, fused_lds))) return rc;
-    if (tb < fused_blocks) {
-      fused_blocks = tb;
-      P = (uint32_t)fused_blocks * 256u;
     }
   }
   const uint32_t cpp1 = S1 / K + (S1 == ss && ss % K ? 1u : 0u);  // no tail: ceil(ss / K)

@@ -53,7 +53,7 @@ def test_tail_phase_is_bitwise(rt, gpu, name, monkeypatch):
     """The two-phase chunk plan (rt_path.h chunk_pixel: the last samples of every pixel in
     shorter chunks after all first-phase chunks) regroups samples only; with exact
     fixed-point pixel sums the image is the same bits for any tail fraction and tail chunk
-    size, and for the one-phase plan (Cornell: the record-loop kernel's TAIL variant)."""
+    size, and for the one-phase plan (the record-loop kernel ignores the request)."""
     t, cam, w, l = _scene(rt, name, 48, 64)
     with rt.Scene(t, w, l) as sc:
         monkeypatch.setenv("RT_TAIL_FRAC", "0")
