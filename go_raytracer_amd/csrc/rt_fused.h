@@ -149,6 +149,10 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
   const SampleAcc sa = {&lacc[threadIdx.x]};
   Path s;
   s.pushes = 0;
+  if constexpr (FT == 0u && TREE == 0) {  // read by split_samples before a lane's first chunk
+    s.chunk = s.j = 0u;
+    s.flags = 0u;
+  }
 #ifdef RT_WAVE_SEGS
   uint32_t wave_segs = 0;  // segments shaded by this wave (wave-uniform: no VGPR)
 #else
@@ -170,9 +174,15 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
   PH_T(t_loop);
   for (;;) {
     PH_T(t_grab);
-    const uint32_t c = grab_chunk(P, b, !has);
+    uint32_t c = grab_chunk(P, b, !has), j0 = 0u, n0 = 0u;
+    // the lean record-loop kernel (C2) shares samples in its drain (split_samples)
+    constexpr bool kSplit = FT == 0u && TREE == 0;
+    if constexpr (kSplit)
+      if (b.part >= (uint32_t)kMaxParts) split_samples(P, s, has, c, j0, n0);
     if (c != 0xFFFFFFFFu) {
-      start_sample<false, cam_mode(FT), FT == 0u && TREE == 0>(P, slot, s, c, 0);
+      start_sample<false, cam_mode(FT), kSplit>(P, slot, s, c, j0);
+      if constexpr (kSplit)
+        if (j0) s.flags = F_SPLIT | (n0 << kCountShift);
       trav_init<FT>(P.sc, s.o, s.d, s.time, tr);
       has = true;
     }

@@ -24,6 +24,10 @@ enum : uint32_t { F_PEND = 1u, F_PRE = 2u, F_NONFINITE = 4u };
 // Path::flags above this bit: the sample count of the path's chunk (chunk_ids().count, set
 // when the chunk starts), so the per-sample "last sample?" test needs no launch parameter
 constexpr uint32_t kCountShift = 8;
+// Path::flags bit 7 (kept by next_sample): the path runs samples split off another lane's
+// chunk (k_fused's drain, split_samples); its sums go to the pixel with atomics, not to the
+// chunk's record
+constexpr uint32_t F_SPLIT = 0x80u;
 enum { OUT_DEAD = 0, OUT_ALIVE = 1, OUT_NEED_CHUNK = 2 };
 
 struct Counters {
@@ -71,6 +75,7 @@ struct Params {
   uint32_t grab_min;   // fused: chunks a wave takes per refill of its batch (>= 1)
   uint32_t parts_log2; // fused: the chunk range is split over 2^parts_log2 partitions ...
   uint32_t gran_log2;  // ... interleaved in granules of 2^gran_log2 chunks (grab_chunk)
+  uint32_t split_min;  // fused drain: a lane with >= split_min samples left shares them (0: off)
   unsigned long long* wave_times;  // debug (RT_WAVE_TIMES): per wave {start, end, segments}
   uint32_t recs_lds;   // leaf records cached in LDS after the nodes (stage_nodes)
   uint64_t seed;
@@ -1477,9 +1482,9 @@ struct SampleAcc {
       atomicAdd(&P.accum[2 * (size_t)P.npix + lp], fz);
     }
   }
-  RT_D void flush(const Params& P, uint32_t chunk) const {
+  RT_D void flush(const Params& P, uint32_t chunk, bool split = false) const {
     if (!lds) return;
-    if (P.csum) {
+    if (P.csum && !split) {
       // the chunk's own 32-B record, two plain 16-B stores.  A pixel atomic is performed
       // beyond L2 and completes late, and every later s_waitcnt vmcnt of the wave (the
       // traversal's node loads, the shading's) waited for it: C3 -4.4 %, C2 -2.5 %, C4
@@ -1694,7 +1699,7 @@ RT_D void next_sample(const Params& P, uint32_t slot, Path& s, uint32_t j, const
   s.j = j;
   s.k = 0;
   s.nst = 0;
-  s.flags &= ~((1u << kCountShift) - 1u);  // the chunk's sample count stays
+  s.flags &= ~(F_SPLIT - 1u);  // the chunk's sample count and F_SPLIT stay
   store_ray<SOA>(P, slot, s);
 }
 
@@ -1992,7 +1997,7 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
   if (isnan(L.x) || isnan(L.y) || isnan(L.z)) printf("NAN gpix %u sample %u\n", s.gpix, s.s0 + s.j);
 #endif
   sa.add(P, s.chunk, L);
-  const uint32_t count = s.flags >> kCountShift;  // chunk_ids().count
+  const uint32_t count = s.flags >> kCountShift;  // chunk_ids().count, or a drain split's
   if (s.j + 1 < count) {
     if (!have_rcam)  // a miss, or the depth limit: the camera draw is made here
       rcam = rt_rng_draw(P.seed, s.gpix, s.s0 + s.j + 1, RT_STREAM_CAMERA);
@@ -2000,9 +2005,54 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
     PH_ADD(PH_TERM, t_term);
     return OUT_ALIVE;
   }
-  sa.flush(P, s.chunk);
+  sa.flush(P, s.chunk, FT == 0u && (s.flags & F_SPLIT));
   PH_ADD(PH_TERM, t_term);
   return OUT_NEED_CHUNK;
+}
+
+// the n-th (from 0) set bit of m, n < popcount(m)
+RT_D uint32_t nth_set_bit(unsigned long long m, uint32_t n) {
+  uint32_t pos = 0u;
+#pragma unroll
+  for (uint32_t w = 32u; w > 0u; w >>= 1) {
+    const uint32_t lo = (uint32_t)__popcll(m & ((1ull << w) - 1ull));
+    if (n >= lo) {
+      n -= lo;
+      m >>= w;
+      pos += w;
+    }
+  }
+  return pos;
+}
+
+// Drain of the fused kernel (every chunk handed out, wave-uniform call): the k-th lane
+// without work takes the upper half of the samples left in the k-th lane that has at least
+// P.split_min left after its current one.  Samples are keyed by (pixel, sample) and summed
+// exactly, so who traces them does not change the image; the taker's sums go to the pixel
+// with atomics (F_SPLIT), the giver's chunk record covers the samples it kept.  A taker gets
+// the giver's chunk in `c`, its samples [j0, n0) of it (j0 >= 1), for start_sample.  A giver
+// may be a taker or have given before: the count it passes on is its current one.
+RT_D void split_samples(const Params& P, Path& s, bool has, uint32_t& c, uint32_t& j0,
+                        uint32_t& n0) {
+  const uint32_t cnt = s.flags >> kCountShift;
+  const uint32_t left = has ? cnt - 1u - s.j : 0u;
+  const bool giver = left >= kparams()->split_min;
+  const unsigned long long need = __ballot(!has && c == 0xFFFFFFFFu), give = __ballot(giver);
+  if (!need || !give) return;
+  const uint32_t n_need = (uint32_t)__popcll(need), n_give = (uint32_t)__popcll(give);
+  const bool needs = ((need >> lane_id()) & 1ull) != 0ull;
+  const uint32_t rank = prefix_count(needs ? need : give);
+  const bool taker = needs && rank < n_give;
+  const uint32_t keep = cnt - ((left + 1u) >> 1);  // the giver's new sample count
+  const uint32_t src = taker ? nth_set_bit(give, rank) : lane_id();
+  const uint32_t t_chunk = __shfl(s.chunk, (int)src), t_keep = __shfl(keep, (int)src),
+                 t_cnt = __shfl(cnt, (int)src);
+  if (giver && rank < n_need) s.flags = (s.flags & ((1u << kCountShift) - 1u)) | (keep << kCountShift);
+  if (taker) {
+    c = t_chunk;
+    j0 = t_keep;
+    n0 = t_cnt;
+  }
 }
 
 // Wave-batched work distribution over partitioned counters.  The chunk range is split

@@ -1156,6 +1156,10 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   // scenes that traverse a tree through L1/L2 keep 128 (32 measured C3 +3.7 %, C4 +2.2 %,
   // C5 +2 %: their waves refill more often and spread over more of the image)
   p.grab_min = (uint32_t)std::max(1, env_int("RT_GRAB_MIN", f_lds ? 32 : K <= 8u ? 256 : 128));
+  {  // drain splitting (k_fused's record-loop kernel): share when >= split_min samples are left
+    const int sm = env_int("RT_SPLIT_MIN", 1);
+    p.split_min = sm > 0 ? (uint32_t)sm : 0xFFFFFFFFu;  // 0: off (no lane has that many)
+  }
   // partitioned chunk counters (rt_path.h grab_chunk): 64 partitions interleaved in
   // granules of 256 chunks; progress slices use one counter (their ranges are contiguous)
   p.parts_log2 = (uint32_t)std::min(6, std::max(0, env_int("RT_PARTS_LOG2", 6)));

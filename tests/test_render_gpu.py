@@ -65,6 +65,23 @@ def test_tail_phase_is_bitwise(rt, gpu, name, monkeypatch):
             assert np.array_equal(img, ref, equal_nan=True), (K, tf, tk)
 
 
+@pytest.mark.parametrize("nranks", [1, 8])
+def test_drain_split_is_bitwise(rt, gpu, nranks, monkeypatch):
+    """The record-loop kernel's drain (rt_path.h split_samples): once every chunk is handed
+    out, a lane without work takes the upper half of the samples another lane has left.
+    Samples are keyed by (pixel, sample) and summed exactly, so the image and the segment
+    count are the same with and without splitting, for any threshold and chunk size."""
+    t, cam, w, l = _scene(rt, "cornell", 64, 64)
+    with rt.Scene(t, w, l) as sc:
+        monkeypatch.setenv("RT_SPLIT_MIN", "0")
+        ref, st0 = sc.render(cam, seed=9, rank=0, nranks=nranks)
+        for m, K in (("1", 0), ("2", 0), ("7", 0), ("1", 64), ("3", 32)):
+            monkeypatch.setenv("RT_SPLIT_MIN", m)
+            img, st = sc.render(cam, seed=9, rank=0, nranks=nranks, chunk=K)
+            assert np.array_equal(img, ref, equal_nan=True), (m, K)
+            assert st["segments"] == st0["segments"], (m, K)
+
+
 def test_big_spheres_outside_the_bvh_same_image(rt, gpu, monkeypatch):
     """Spheres of radius >= kBigSphereR are tested before the BVH (trav_init) instead of as
     BVH leaves: the same fp64 test on the same record, so the same closest hits.  book1's
