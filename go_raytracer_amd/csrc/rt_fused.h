@@ -149,7 +149,7 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
   const SampleAcc sa = {&lacc[threadIdx.x]};
   Path s;
   s.pushes = 0;
-  if constexpr (FT == 0u && TREE == 0) {  // read by split_samples before a lane's first chunk
+  if constexpr ((FT == 0u && TREE == 0) || kSplitTrees) {  // read by split_samples before a lane's first chunk
     s.chunk = s.j = 0u;
     s.flags = 0u;
   }
@@ -175,12 +175,13 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
   for (;;) {
     PH_T(t_grab);
     uint32_t c = grab_chunk(P, b, !has), j0 = 0u, n0 = 0u;
-    // the lean record-loop kernel (C2) shares samples in its drain (split_samples)
-    constexpr bool kSplit = FT == 0u && TREE == 0;
+    // lanes share samples in the drain (split_samples; RT_NO_SPLIT_TREES: the record-loop
+    // kernel only)
+    constexpr bool kSplit = (FT == 0u && TREE == 0) || kSplitTrees;
     if constexpr (kSplit)
       if (b.part >= (uint32_t)kMaxParts) split_samples(P, s, has, c, j0, n0);
     if (c != 0xFFFFFFFFu) {
-      start_sample<false, cam_mode(FT), kSplit>(P, slot, s, c, j0);
+      start_sample<false, cam_mode(FT), FT == 0u && TREE == 0>(P, slot, s, c, j0);
       if constexpr (kSplit)
         if (j0) s.flags = F_SPLIT | (n0 << kCountShift);
       trav_init<FT>(P.sc, s.o, s.d, s.time, tr);

@@ -28,6 +28,11 @@ constexpr uint32_t kCountShift = 8;
 // chunk (k_fused's drain, split_samples); its sums go to the pixel with atomics, not to the
 // chunk's record
 constexpr uint32_t F_SPLIT = 0x80u;
+#ifdef RT_NO_SPLIT_TREES
+constexpr bool kSplitTrees = false;  // A/B builds: drain splitting in the record-loop kernel only
+#else
+constexpr bool kSplitTrees = true;
+#endif
 enum { OUT_DEAD = 0, OUT_ALIVE = 1, OUT_NEED_CHUNK = 2 };
 
 struct Counters {
@@ -2005,7 +2010,7 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
     PH_ADD(PH_TERM, t_term);
     return OUT_ALIVE;
   }
-  sa.flush(P, s.chunk, FT == 0u && (s.flags & F_SPLIT));
+  sa.flush(P, s.chunk, (FT == 0u || kSplitTrees) && (s.flags & F_SPLIT));
   PH_ADD(PH_TERM, t_term);
   return OUT_NEED_CHUNK;
 }

@@ -65,13 +65,15 @@ def test_tail_phase_is_bitwise(rt, gpu, name, monkeypatch):
             assert np.array_equal(img, ref, equal_nan=True), (K, tf, tk)
 
 
-@pytest.mark.parametrize("nranks", [1, 8])
-def test_drain_split_is_bitwise(rt, gpu, nranks, monkeypatch):
-    """The record-loop kernel's drain (rt_path.h split_samples): once every chunk is handed
-    out, a lane without work takes the upper half of the samples another lane has left.
-    Samples are keyed by (pixel, sample) and summed exactly, so the image and the segment
-    count are the same with and without splitting, for any threshold and chunk size."""
-    t, cam, w, l = _scene(rt, "cornell", 64, 64)
+@pytest.mark.parametrize("name,nranks", [("cornell", 1), ("cornell", 8), ("cornell_smoke", 8),
+                                          ("book1", 8), ("book2", 8)])
+def test_drain_split_is_bitwise(rt, gpu, name, nranks, monkeypatch):
+    """The fused kernels' drain (rt_path.h split_samples): once every chunk is handed out, a
+    lane without work takes the upper half of the samples another lane has left.  Samples
+    are keyed by (pixel, sample) and summed exactly, so the image and the segment count are
+    the same with and without splitting, for any threshold and chunk size (the record loop,
+    with media, and the BVH kernels of book1 and book2)."""
+    t, cam, w, l = _scene(rt, name, 64, 64)
     with rt.Scene(t, w, l) as sc:
         monkeypatch.setenv("RT_SPLIT_MIN", "0")
         ref, st0 = sc.render(cam, seed=9, rank=0, nranks=nranks)
