@@ -19,6 +19,7 @@ from ._lib import (RT_FT_ALL, RT_FT_BOX, RT_NOISE_MARBLE, RT_NOISE_PERLIN,  # no
                    check, lib)
 
 __all__ = ["Tree", "Camera", "Scene", "quantize", "format_ppm", "device_count", "RtError",
+           "tune", "untune", "tuning", "tune_knobs", "tune_from_env",
            "demo_scene", "DEMO_SCENES", "LoadObjOptions", "DefaultLoadOptions", "quantize_device",
            "format_ppm_device"]
 
@@ -587,3 +588,53 @@ def format_ppm_device(rgb, to_host=True):
 
 def device_count():
     return lib().rt_device_count()
+
+
+# ---- tuning knobs (rt_tune_set): the library never reads the process environment ----
+def tune_knobs():
+    """{knob name: changes_image_bits} for every knob the library consults."""
+    n = lib().rt_tune_list(-1, None, None)
+    out = {}
+    for i in range(n):
+        name, bits = C.c_char_p(), C.c_int32()
+        check(lib().rt_tune_list(i, C.byref(name), C.byref(bits)))
+        out[name.value.decode()] = bool(bits.value)
+    return out
+
+
+def tune(name, value):
+    """Set knob `name` (e.g. "RT_TAIL_FRAC") to `value`; None clears it."""
+    v = None if value is None else str(value).encode()
+    check(lib().rt_tune_set(name.encode(), v))
+
+
+def untune(name=None):
+    """Clear one knob, or every knob (name None)."""
+    check(lib().rt_tune_set(None if name is None else name.encode(), None))
+
+
+class tuning:
+    """Context manager: ``with rt.tuning(RT_SPLIT_MIN=0): ...`` sets knobs, then clears them."""
+
+    def __init__(self, **knobs):
+        self.knobs = knobs
+
+    def __enter__(self):
+        for k, v in self.knobs.items():
+            tune(k, v)
+        return self
+
+    def __exit__(self, *a):
+        for k in self.knobs:
+            untune(k)
+
+
+def tune_from_env(environ=None):
+    """Dev tools only (tools/*): copy RT_* knobs from the environment into the library, an
+    explicit opt-in of the calling process.  Returns the knobs set."""
+    import os
+    env = os.environ if environ is None else environ
+    got = {k: env[k] for k in tune_knobs() if env.get(k)}
+    for k, v in got.items():
+        tune(k, v)
+    return got

@@ -62,7 +62,8 @@ class RtSceneInfo(C.Structure):
         "n_spheres", "n_quads", "n_triangles", "n_world_prims", "n_media",
         "n_lights", "n_bvh_nodes", "bvh_depth", "max_leaf", "n_materials",
         "n_textures", "n_images", "n_perlins", "medium_draws")] + [
-        ("device_bytes", C.c_int64), ("features", C.c_int32), ("bvh_builder", C.c_int32)]
+        ("device_bytes", C.c_int64), ("features", C.c_int32), ("bvh_builder", C.c_int32),
+        ("tuned", C.c_int32), ("_pad", C.c_int32)]
 
 
 class RtRenderOpts(C.Structure):
@@ -89,6 +90,7 @@ class RtStats(C.Structure):
         ("tree_width", C.c_int32), ("lds_scene", C.c_int32),
         ("chunk_samples", C.c_int32), ("record_boxes", C.c_int32),
         ("overflow_samples", C.c_uint64),
+        ("tuned", C.c_int32), ("chunk_records", C.c_int32),
     ]
 
 
@@ -134,6 +136,8 @@ _DP = C.POINTER(C.c_double)
 SIGNATURES = {
     "rt_last_error": (C.c_char_p, []),
     "rt_abi_version": (_I, []),
+    "rt_tune_set": (_I, [C.c_char_p, C.c_char_p]),
+    "rt_tune_list": (_I, [C.c_int32, C.POINTER(C.c_char_p), C.POINTER(C.c_int32)]),
     "rt_tree_create": (_I, [C.POINTER(_P)]),
     "rt_tree_destroy": (_I, [_P]),
     "rt_tree_seed": (_I, [_P, C.c_uint64]),

@@ -54,15 +54,7 @@ struct TmpNode {
 };
 
 constexpr int kBins = 16;
-// SAH leaf/split trade-off; RT_BVH_LEAF / RT_BVH_CT / RT_BVH_CI override (tuning)
-static int env_i(const char* n, int d) {
-  const char* e = getenv(n);
-  return e && *e ? atoi(e) : d;
-}
-static double env_d(const char* n, double d) {
-  const char* e = getenv(n);
-  return e && *e ? atof(e) : d;
-}
+// SAH leaf/split trade-off; the knobs RT_BVH_LEAF / RT_BVH_CT / RT_BVH_CI override (rt_tune_set)
 
 }  // namespace
 
@@ -74,8 +66,8 @@ int build_bvh(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi
   // of up to 4; trees read through L1/L2 (C3 485 prims, C4 3.4k, C5 1M) with single-prim
   // leaves (C4/C5 -11 %, C3 -1.6 %), the parent's child box culling each prim before its
   // record is fetched.  Above 256 prims a tree no longer fits the LDS cache.
-  const int kLeafTarget = std::min(env_i("RT_BVH_LEAF", n > 256 ? 1 : 4), MAX_LEAF);
-  const double kCostTrav = env_d("RT_BVH_CT", 1.0), kCostIsect = env_d("RT_BVH_CI", 1.0);
+  const int kLeafTarget = std::min(tune_int("RT_BVH_LEAF", n > 256 ? 1 : 4), MAX_LEAF);
+  const double kCostTrav = tune_num("RT_BVH_CT", 1.0), kCostIsect = tune_num("RT_BVH_CI", 1.0);
   s.nodes.clear();
   s.refs.clear();
   s.prim_bounds.clear();
@@ -100,7 +92,7 @@ int build_bvh(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi
   }
   std::vector<int> idx(n);
   for (int i = 0; i < n; ++i) idx[i] = i;
-  const bool timing = getenv("RT_TIMING") != nullptr;
+  const bool timing = tune_int("RT_TIMING", 0) != 0;
   auto tic = std::chrono::steady_clock::now();
   auto lap = [&](const char* what) {
     if (!timing) return;
@@ -112,7 +104,8 @@ int build_bvh(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi
   // Node split: bounds, binned SAH over three axes, partition of idx[first,
   // first+count).  Box growth is min/max and bin counts are integers, so running
   // the loops on T threads (large nodes) gives bit-identical trees.
-  const int threads = std::max(1, std::min(env_i("RT_THREADS", env_i("OMP_NUM_THREADS", 16)),
+  // (bit-identical for any thread count: 16, the GPU box's CPU share, unless RT_THREADS is set)
+  const int threads = std::max(1, std::min(tune_int("RT_THREADS", 16),
                                            (int)std::max(1u, std::thread::hardware_concurrency())));
   auto par = [&](int T, int first, int count, auto&& fn) {  // fn(t, lo, hi)
     if (T <= 1) {

@@ -570,13 +570,11 @@ int flatten_scene(const Tree& t, int world, int lights, HostScene& out) {
     return set_error(RT_ERR_INVALID, "rt_scene_create: bad world handle %d", world);
   if (lights >= (int)t.nodes.size())
     return set_error(RT_ERR_INVALID, "rt_scene_create: bad lights handle %d", lights);
-  const bool timing = getenv("RT_TIMING") != nullptr;
+  const bool timing = tune_int("RT_TIMING", 0) != 0;
   auto t0 = std::chrono::steady_clock::now();
   Flattener f(t, out);
-  const char* bl = getenv("RT_BOX_LEAVES");
-  f.box_leaves_on = !(bl && *bl && atoi(bl) == 0);
-  const char* bsr = getenv("RT_BIG_SPHERE_R");  // A/B: a huge value keeps every sphere in the BVH
-  f.big_r = bsr && *bsr ? atof(bsr) : kBigSphereR;
+  f.box_leaves_on = tune_int("RT_BOX_LEAVES", 1) != 0;
+  f.big_r = tune_num("RT_BIG_SPHERE_R", kBigSphereR);  // A/B: a huge value keeps every sphere in the BVH
   int rc = f.walk(world, Xf{}, 1, 0);
   if (timing)
     fprintf(stderr, "[rt] flatten walk %.3f s\n",
@@ -637,16 +635,15 @@ int flatten_scene(const Tree& t, int world, int lights, HostScene& out) {
   // keep prim bounds for export, in the BVH's final ref order (set by build_bvh)
   t0 = std::chrono::steady_clock::now();
   // large scenes: PLOC on the GPU (rt_build.hip) when a device is present
-  const char* bsel = getenv("RT_BVH_BUILDER");
-  const std::string builder = bsel ? bsel : "auto";
-  const char* bmin = getenv("RT_BVH_DEVICE_MIN");
-  const size_t dev_min = bmin && *bmin ? (size_t)atol(bmin) : (size_t)65536;
+  std::string builder = "auto";
+  tune_str("RT_BVH_BUILDER", &builder);
+  const size_t dev_min = (size_t)tune_num("RT_BVH_DEVICE_MIN", 65536.0);
   const bool on_device =
       f.world_refs.size() >= 2 &&
       (builder == "device" || (builder == "auto" && f.world_refs.size() >= dev_min)) &&
       bvh_device_available();
   if (builder == "device" && !on_device && f.world_refs.size() >= 2)
-    return set_error(RT_ERR_DEVICE, "RT_BVH_BUILDER=device but no HIP device is available");
+    return set_error(RT_ERR_DEVICE, "RT_BVH_BUILDER device: no HIP device is available");
   out.bvh_builder = on_device ? 1 : 0;
   rc = on_device ? build_bvh_device(out, f.lo, f.hi, f.world_refs, -1)  // current device
                  : build_bvh(out, f.lo, f.hi, f.world_refs);
@@ -656,8 +653,7 @@ int flatten_scene(const Tree& t, int world, int lights, HostScene& out) {
   if (rc != RT_OK) return rc;
   // the wide tree (host_bvh8.cpp), opt-in: RT_BVH8=1 at scene creation.  Measured
   // slower than the BVH4 on C4/C5, kept for A/B and further work
-  const char* b8 = getenv("RT_BVH8");
-  if (b8 && atoi(b8) != 0 && out.refs.size() >= kBvh8MinRefs) {
+  if (tune_int("RT_BVH8", 0) != 0 && out.refs.size() >= kBvh8MinRefs) {
     t0 = std::chrono::steady_clock::now();
     rc = build_bvh8(out);
     if (rc != RT_OK) {

@@ -18,7 +18,7 @@ static uint32_t fbits_host(float f) {
 // the materials of those prims and media, and the textures of those materials
 // (through checker children).  Materials and textures that are built but never
 // placed (book1's perlin orbs, main.go:52-60) do not count, so such a scene runs a
-// leaner kernel.  RT_FEATURES_ALL=1 counts every table entry (A/B).
+// leaner kernel.  The knob RT_FEATURES_ALL=1 counts every table entry (A/B).
 // *noise_table0: every reachable noise texture uses perlin table 0, the one the
 // feature-set kernels stage in LDS (others need the all-features kernel).
 uint32_t scene_features(const HostScene& h, bool* noise_table0) {
@@ -62,8 +62,7 @@ uint32_t scene_features(const HostScene& h, bool* noise_table0) {
   for (const DevLight& l : h.lights) prim(l.ref);
   if (!h.media.empty()) f |= FT_MEDIA;
   for (const DevMedium& m : h.media) use_mat(m.phase_mat);
-  const char* all = getenv("RT_FEATURES_ALL");
-  const bool every = all && *all && atoi(all) != 0;
+  const bool every = tune_int("RT_FEATURES_ALL", 0) != 0;
   std::vector<char> tex_used(h.texs.size(), 0);
   std::vector<int> st;
   for (size_t i = 0; i < h.mats.size(); ++i) {
@@ -110,6 +109,7 @@ int rt_scene_create(const rt_tree* t, int world, int lights, rt_scene** out) {
     return rc;
   }
   s->s.h.features = rt::scene_features(s->s.h, &s->s.h.noise_table0);  // walks every prim: once, not per render
+  s->s.h.tuned = rt::tune_count();
   *out = s;
   return RT_OK;
 }
@@ -150,6 +150,7 @@ int rt_scene_info_get(const rt_scene* sc, rt_scene_info* o) {
   o->device_bytes = b;
   o->features = (int32_t)h.features;
   o->bvh_builder = h.bvh_builder;
+  o->tuned = h.tuned;
   return RT_OK;
 }
 

@@ -445,7 +445,7 @@ int model(rt_tree* t, const char* asset_dir, rt_camera* c, int* world_out, int* 
     fclose(f);
     CHECK(rt_load_obj(t, path.c_str(), &opt, &mdl, &lights, nullptr));
   } else {
-    const bool timing = getenv("RT_TIMING") != nullptr;
+    const bool timing = rt::tune_int("RT_TIMING", 0) != 0;
     auto t0 = std::chrono::steady_clock::now();
     std::string obj = substitute_dragon_obj(nu < 0 ? 2048 : nu, nv < 0 ? 256 : nv);
     auto t1 = std::chrono::steady_clock::now();

@@ -441,7 +441,7 @@ int build_bvh_device(HostScene& s, const std::vector<F4>& lo, const std::vector<
   const int n = (int)prims.size();
   if (n < 2) return set_error(RT_ERR_INVALID, "build_bvh_device: needs 2+ prims");
   if ((uint32_t)n > 0x7FFFFFFu) return set_error(RT_ERR_UNSUPPORTED, "too many prims (%d)", n);
-  const bool timing = getenv("RT_TIMING") != nullptr;
+  const bool timing = tune_int("RT_TIMING", 0) != 0;
   auto t0 = std::chrono::steady_clock::now();
   // device < 0: the calling thread's current device (one process per GPU builds on its
   // own GPU); the caller's current device is restored on return
@@ -499,8 +499,7 @@ int build_bvh_device(HostScene& s, const std::vector<F4>& lo, const std::vector<
   // PLOC iterations down to `top` clusters; the top of the tree is then built on
   // the host by a full SAH sweep over those clusters (PLOC's radius-limited merges
   // are weakest where few large clusters remain)
-  const char* tenv = getenv("RT_BVH_TOP");
-  const int top = std::max(1, tenv && *tenv ? atoi(tenv) : PLOC_TOP);
+  const int top = std::max(1, tune_int("RT_BVH_TOP", PLOC_TOP));
   int m = n, node_base = n, cur = 0, iters = 0, force = 0;
   while (m > top) {
     if (++iters > 4 * 64 + n) return set_error(RT_ERR_DEVICE, "bvh build: no progress");

@@ -17,6 +17,13 @@ namespace rt {
 // thread-local error slot (rt_last_error)
 int set_error(int code, const char* fmt, ...);
 
+// host_tune.cpp: tuning overrides set by the caller through rt_tune_set (the library never
+// reads the process environment).  The value of knob `name`, or `dflt` when it is not set.
+bool tune_str(const char* name, std::string* out);
+double tune_num(const char* name, double dflt);
+int tune_int(const char* name, int dflt);
+int32_t tune_count();  // knobs currently set (rt_scene_info.tuned, rt_stats.tuned)
+
 struct Tree {
   // nodes as created; LIST/BVH children live in lists[node.a]
   std::vector<rt_node> nodes;
@@ -75,6 +82,7 @@ struct HostScene {
   int32_t bvh_builder = 0;  // 0 host binned SAH, 1 device PLOC
   uint32_t features = 0;    // scene_features(), computed once by rt_scene_create
   bool noise_table0 = true; // every reachable noise texture uses perlin table 0 (scene_features)
+  int32_t tuned = 0;        // tuning knobs set when the scene was created (rt_scene_info.tuned)
 };
 
 struct DeviceScene;  // defined in the HIP translation unit

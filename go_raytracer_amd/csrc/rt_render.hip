@@ -322,11 +322,9 @@ static int upload(DeviceScene* ds, const std::vector<T>& v, const T** out) {
   return RT_OK;
 }
 
-// scheduling knobs of the fused kernel (A/B experiments; defaults measured)
-static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e && *e ? atoi(e) : dflt;
-}
+// scheduling knobs of the fused kernel (A/B experiments; defaults measured): rt_tune_set
+// only, never the process environment (host_tune.cpp)
+static int env_int(const char* name, int dflt) { return tune_int(name, dflt); }
 
 
 static FastDiv make_fastdiv(uint32_t d) {
@@ -414,7 +412,7 @@ static int ensure_scene(Scene* s, int device, DeviceScene** out) {
   ds->device = device;
   const auto t0 = std::chrono::steady_clock::now();
   const int rc = upload_scene(s, ds);
-  if (getenv("RT_TIMING"))
+  if (tune_int("RT_TIMING", 0))
     fprintf(stderr, "[rt] scene upload to device %d %.3f s\n", device,
             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
   if (rc != RT_OK) {
@@ -857,10 +855,14 @@ static const void* pick_fused(bool lds, uint32_t set, int tree) {
   if (tree == 0 && !lds && set == kFtSets[1]) return (const void*)k_fused<false, kFtSets[1], 0>;
   if (tree == 2 && lds && set == kFtSets[0]) return (const void*)k_fused<true, kFtSets[0], 2>;
   if (tree == 2 && lds && set == kFtSets[1]) return (const void*)k_fused<true, kFtSets[1], 2>;
-  if (tree == 8 && !lds) {  // BVH8: large trees read through L1/L2, the three tree sets
-    if (set == kFtSets[2]) return (const void*)k_fused<false, kFtSets[2], 8>;
-    if (set == kFtSets[3]) return (const void*)k_fused<false, kFtSets[3], 8>;
-    if (set == kFtSets[4]) return (const void*)k_fused<false, kFtSets[4], 8>;
+  if (tree == 8) {
+#ifdef RT_BVH8_KERNELS
+    // BVH8 (measured slower than the BVH4): A/B builds only.  Large trees
+    // read through L1/L2, the three tree sets
+    if (!lds && set == kFtSets[2]) return (const void*)k_fused<false, kFtSets[2], 8>;
+    if (!lds && set == kFtSets[3]) return (const void*)k_fused<false, kFtSets[3], 8>;
+    if (!lds && set == kFtSets[4]) return (const void*)k_fused<false, kFtSets[4], 8>;
+#endif
     return nullptr;
   }
   if (tree != 4) return nullptr;  // no such kernel: render_impl never asks (see tree there)
@@ -887,6 +889,7 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   int rc = rt_camera_derive(cam, &cd);
   if (rc) return rc;
   auto t_start = std::chrono::steady_clock::now();
+  const int32_t tuned = tune_count();  // rt_stats.tuned: knobs off their defaults
 
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
@@ -1059,16 +1062,41 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
       st->ostack_cols = cols;
     }
   }
-  // fused: the per-chunk sums (32 B per chunk, every record stored once per render: no clear)
-  const bool use_csum = mode == RT_MODE_FUSED && env_int("RT_CSUM", 1) != 0;
-  if (use_csum && st->csum_chunks < n_chunks) {
-    if (st->csum) {
+  // fused: the per-chunk sums (32 B per chunk, every record stored once per render: no clear).
+  // The buffer grows with the sample count, not the image: above its cap (RT_CSUM_MAX_MB,
+  // default 16 GiB, and at most half of the device's free memory) or when it cannot be
+  // allocated, the render falls back to pixel atomics (P.csum == nullptr: the same integer
+  // sums, so the same image; rt_stats.chunk_records = 0).  A buffer more than 4x larger than
+  // this render needs (and over 256 MiB) is released first.
+  bool use_csum = mode == RT_MODE_FUSED && env_int("RT_CSUM", 1) != 0;
+  {
+    const size_t need_b = 32 * (size_t)n_chunks;
+    auto drop_csum = [&]() -> int {
+      if (!st->csum) return RT_OK;
       HIP_OK(hipFree(st->csum));
       st->allocs.erase(std::find(st->allocs.begin(), st->allocs.end(), (void*)st->csum));
       st->csum = nullptr;
+      st->csum_chunks = 0;
+      return RT_OK;
+    };
+    if (st->csum && (!use_csum || (st->csum_chunks > 4 * (size_t)n_chunks &&
+                                   32 * st->csum_chunks > ((size_t)256 << 20))))
+      if ((rc = drop_csum())) return rc;
+    if (use_csum && st->csum_chunks < n_chunks) {
+      if ((rc = drop_csum())) return rc;
+      size_t free_b = 0, total_b = 0;
+      const size_t cap_b = (size_t)std::max(0, env_int("RT_CSUM_MAX_MB", 16384)) << 20;
+      if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+      void* q = nullptr;
+      if (need_b <= cap_b && need_b <= free_b / 2 && hipMalloc(&q, std::max<size_t>(need_b, 32)) == hipSuccess) {
+        st->allocs.push_back(q);
+        st->csum = (unsigned long long*)q;
+        st->csum_chunks = n_chunks;
+      } else {
+        (void)hipGetLastError();  // a failed allocation is not sticky: pixel atomics instead
+        use_csum = false;
+      }
     }
-    if ((rc = dalloc(st, &st->csum, 4 * (size_t)n_chunks))) return rc;
-    st->csum_chunks = n_chunks;
   }
 
   hipStream_t stream = (hipStream_t)o.stream;
@@ -1275,7 +1303,8 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     }
     // debug: per-wave start/end clocks (100 MHz), segments and (RT_PHASES builds) phase
     // cycles -> binary file RT_WAVE_TIMES, kWaveRec u64 per wave
-    const char* wt_path = getenv("RT_WAVE_TIMES");
+    std::string wt_file;
+    const char* wt_path = tune_str("RT_WAVE_TIMES", &wt_file) ? wt_file.c_str() : nullptr;
     unsigned long long* wt = nullptr;
     const size_t n_waves = (size_t)fused_blocks * 4;
     if (wt_path && *wt_path) {
@@ -1393,6 +1422,8 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     stats->tree_width = tree;
     stats->chunk_samples = (int32_t)K;
     stats->record_boxes = tree == 0 ? ds->brute_boxes : 0;
+    stats->tuned = tuned;
+    stats->chunk_records = p.csum ? 1 : 0;
     stats->lds_scene = mode == RT_MODE_FUSED ? (f_lds ? 1 : 0) : (lds_nodes ? 1 : 0);
     auto sum_ms = [&](const std::vector<std::pair<int, int>>& v, double* acc) -> int {
       for (auto& pr : v) {

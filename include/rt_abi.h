@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 enum {
   RT_OK = 0,
@@ -38,6 +38,18 @@ enum {
 
 const char* rt_last_error(void);
 int rt_abi_version(void);
+
+/* Tuning overrides (A/B experiments and tests; the knobs and their measured defaults are
+ * listed in DESIGN.md §6).  The library never reads the process environment: a knob
+ * differs from its default only after the caller sets it here, and rt_scene_info.tuned /
+ * rt_stats.tuned report how many knobs were set when the scene was created / the render
+ * ran (the reference is configured through Camera fields only, camera.go:181-207).
+ * value: a number as text (or a file path for RT_WAVE_TIMES); NULL clears the knob;
+ * name NULL clears every knob.  Unknown names return RT_ERR_INVALID.  Process-wide. */
+int rt_tune_set(const char* name, const char* value);
+/* Knob i's name and whether it may change image bits (the others move work only); returns
+ * the number of knobs (i < 0: just the count). */
+int rt_tune_list(int32_t i, const char** name, int32_t* changes_bits);
 
 /* ------------------------------------------------------------------------ */
 /* Scene tree: one constructor per reference constructor.                    */
@@ -269,8 +281,8 @@ typedef struct rt_scene rt_scene;
  * and build the device BVH (BuildBVH bvh.go:21-61 + the world list).  Scenes of
  * >= 65536 world prims build it on the calling thread's current HIP device (PLOC,
  * DESIGN.md "BVH"; the current device is left unchanged) when one is
- * present, otherwise with the host binned-SAH builder; RT_BVH_BUILDER=host|device
- * overrides, RT_BVH_DEVICE_MIN moves the threshold.  lights may be -1. */
+ * present, otherwise with the host binned-SAH builder; the knobs RT_BVH_BUILDER
+ * (host|device) and RT_BVH_DEVICE_MIN (rt_tune_set) override.  lights may be -1. */
 int rt_scene_create(const rt_tree* t, int world, int lights, rt_scene** out);
 int rt_scene_destroy(rt_scene* s);
 
@@ -283,6 +295,8 @@ typedef struct {
   int64_t device_bytes; /* scene bytes uploaded to HBM */
   int32_t features;     /* RT_FT_* bits the scene needs (selects the fused kernel) */
   int32_t bvh_builder;  /* 0: host binned SAH, 1: device PLOC (rt_scene_create) */
+  int32_t tuned;        /* rt_tune_set knobs set when the scene was created (0: defaults) */
+  int32_t _pad;
 } rt_scene_info;
 
 /* scene features (rt_scene_info.features, rt_stats.kernel_features) */
@@ -370,6 +384,9 @@ typedef struct {
   /* sample channels with |v| >= 2^31 / spp_sqrt^2 (outside the exact fixed-point pixel
    * sum; added in fp64 instead — the image is then order-dependent in those pixels) */
   uint64_t overflow_samples;
+  int32_t tuned;           /* rt_tune_set knobs set when the render ran (0: defaults) */
+  int32_t chunk_records;   /* 1: per-chunk sum records, 0: pixel atomics (record buffer
+                              over its cap or not allocatable: same image) */
 } rt_stats;
 
 /* Render this rank's rows; out_rgb (host) receives linear mean RGB

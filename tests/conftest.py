@@ -27,6 +27,14 @@ def oracle():
     return pyoracle
 
 
+@pytest.fixture
+def tune(rt):
+    """Set tuning knobs for one test (rt_tune_set); every knob is cleared afterwards."""
+    rt.untune()
+    yield rt.tune
+    rt.untune()
+
+
 @pytest.fixture(scope="session")
 def gpu(rt):
     n = rt.device_count()

@@ -33,7 +33,9 @@ def test_bindings_cover_header(rt):
 
 
 def test_abi_version(rt):
-    assert rt.lib().rt_abi_version() == 2  # 2: rt_render_multi, rt_stats.overflow_samples
+    # 2: rt_render_multi, rt_stats.overflow_samples; 3: rt_tune_set (no environment reads),
+    # rt_scene_info.tuned, rt_stats.tuned / chunk_records
+    assert rt.lib().rt_abi_version() == 3
 
 
 @pytest.mark.skipif(shutil.which("gcc") is None, reason="no C compiler")
@@ -85,3 +87,59 @@ def test_render_multi_argument_errors(rt):
     with rt.Scene(t, w, l) as sc:
         with pytest.raises(rt.RtError):
             sc.render_multi(cam, [])
+
+
+def _all_knobs_off_default(rt):
+    """A non-default value for every knob the library knows (rt_tune_list)."""
+    odd = {"RT_BVH_BUILDER": "host", "RT_WAVE_TIMES": "/nonexistent/wt.bin", "RT_BIG_SPHERE_R": "1e30",
+           "RT_BVH_CT": "3.5", "RT_BVH_CI": "0.25", "RT_THREADS": "3"}
+    return {k: odd.get(k, "0" if k not in ("RT_TREE", "RT_BVH8", "RT_FEATURES_ALL", "RT_TIMING")
+                       else "1") for k in rt.tune_knobs()}
+
+
+def _scene_state(rt, name):
+    t, cam, w, l = rt.demo_scene(name)
+    with rt.Scene(t, w, l) as sc:
+        info = sc.info()
+        nodes, refs, root, bounds = sc.export_bvh()
+        return info, nodes.tobytes(), refs.tobytes(), root, sc.export_bvh8()[0].size
+
+
+@pytest.mark.parametrize("name", ["cornell", "book2", "book1"])
+def test_environment_does_not_configure_the_library(rt, name, monkeypatch):
+    """the library reads no RT_* environment variable.  With every knob
+    set to a non-default value in the environment, a scene's info, BVH and kernel features
+    are those of a clean environment, and it reports no tuning (rt_scene_info.tuned = 0)."""
+    base = _scene_state(rt, name)
+    assert base[0]["tuned"] == 0
+    knobs = _all_knobs_off_default(rt)
+    assert len(knobs) >= 30
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("RT_BVH_BUILDER", "device")  # would fail without a GPU if it were read
+    assert _scene_state(rt, name) == base
+
+
+def test_tuning_is_explicit_and_reported(rt, tune):
+    """Knobs change behaviour only through rt_tune_set, and the scene reports them."""
+    assert rt.tune_knobs()["RT_BOX_LEAVES"] is True  # changes image bits
+    assert rt.tune_knobs()["RT_STEP_BUDGET"] is False  # moves work only
+    with pytest.raises(rt.RtError):
+        rt.tune("RT_NOT_A_KNOB", 1)
+    t, cam, w, l = rt.demo_scene("book1")  # its perlin orbs are built but never placed
+    with rt.Scene(t, w, l) as sc:
+        feats = sc.info()["features"]
+    tune("RT_FEATURES_ALL", 1)
+    tune("RT_TIMING", 0)
+    t, cam, w, l = rt.demo_scene("book1")
+    with rt.Scene(t, w, l) as sc:
+        info = sc.info()
+    assert info["tuned"] == 2 and info["features"] != feats
+    rt.untune()
+    with rt.tuning(RT_BVH_LEAF=2):
+        t, cam, w, l = rt.demo_scene("book1")
+        with rt.Scene(t, w, l) as sc:
+            assert sc.info()["tuned"] == 1
+    t, cam, w, l = rt.demo_scene("book1")
+    with rt.Scene(t, w, l) as sc:
+        assert sc.info()["tuned"] == 0

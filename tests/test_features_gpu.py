@@ -58,7 +58,7 @@ def test_noise_tables_kernel_choice(rt, oracle, gpu, tables):
     assert m["q_equal"] >= 0.995, m
 
 
-def test_box_leaves_match_per_quad_faces(rt, oracle, gpu, monkeypatch):
+def test_box_leaves_match_per_quad_faces(rt, oracle, gpu, tune):
     """Box leaves (one slab test per NewBox, rt_kernels.h hit_box_rec) against the same
     scene built with the six quads as leaves (RT_BOX_LEAVES=0): the two differ only
     where the slab and the quad tests round differently at box edges, and both meet P1
@@ -68,7 +68,7 @@ def test_box_leaves_match_per_quad_faces(rt, oracle, gpu, monkeypatch):
     with rt.Scene(t, w, l) as sc:
         assert sc.info()["features"] & rt.RT_FT_BOX
         on, st_on = sc.render(cam, seed=4)
-    monkeypatch.setenv("RT_BOX_LEAVES", "0")
+    tune("RT_BOX_LEAVES", "0")
     with rt.Scene(t, w, l) as sc:
         assert not sc.info()["features"] & rt.RT_FT_BOX
         off, st_off = sc.render(cam, seed=4)

@@ -49,25 +49,25 @@ def test_bitwise_invariances(rt, gpu, name):
 
 
 @pytest.mark.parametrize("name", ["book1", "book2", "cornell"])
-def test_tail_phase_is_bitwise(rt, gpu, name, monkeypatch):
+def test_tail_phase_is_bitwise(rt, gpu, name, tune):
     """The two-phase chunk plan (rt_path.h chunk_pixel: the last samples of every pixel in
     shorter chunks after all first-phase chunks) regroups samples only; with exact
     fixed-point pixel sums the image is the same bits for any tail fraction and tail chunk
     size, and for the one-phase plan (the record-loop kernel ignores the request)."""
     t, cam, w, l = _scene(rt, name, 48, 64)
     with rt.Scene(t, w, l) as sc:
-        monkeypatch.setenv("RT_TAIL_FRAC", "0")
+        tune("RT_TAIL_FRAC", "0")
         ref, _ = sc.render(cam, seed=6)
         for K, tf, tk in ((32, "4", "4"), (32, "8", "3"), (16, "2", "5"), (8, "4", "1")):
-            monkeypatch.setenv("RT_TAIL_FRAC", tf)
-            monkeypatch.setenv("RT_TAIL_K", tk)
+            tune("RT_TAIL_FRAC", tf)
+            tune("RT_TAIL_K", tk)
             img, _ = sc.render(cam, seed=6, chunk=K)
             assert np.array_equal(img, ref, equal_nan=True), (K, tf, tk)
 
 
 @pytest.mark.parametrize("name,nranks", [("cornell", 1), ("cornell", 8), ("cornell_smoke", 8),
                                           ("book1", 8), ("book2", 8)])
-def test_drain_split_is_bitwise(rt, gpu, name, nranks, monkeypatch):
+def test_drain_split_is_bitwise(rt, gpu, name, nranks, tune):
     """The fused kernels' drain (rt_path.h split_samples): once every chunk is handed out, a
     lane without work takes the upper half of the samples another lane has left.  Samples
     are keyed by (pixel, sample) and summed exactly, so the image and the segment count are
@@ -75,27 +75,41 @@ def test_drain_split_is_bitwise(rt, gpu, name, nranks, monkeypatch):
     with media, and the BVH kernels of book1 and book2)."""
     t, cam, w, l = _scene(rt, name, 64, 64)
     with rt.Scene(t, w, l) as sc:
-        monkeypatch.setenv("RT_SPLIT_MIN", "0")
+        tune("RT_SPLIT_MIN", "0")
         ref, st0 = sc.render(cam, seed=9, rank=0, nranks=nranks)
         for m, K in (("1", 0), ("2", 0), ("7", 0), ("1", 64), ("3", 32)):
-            monkeypatch.setenv("RT_SPLIT_MIN", m)
+            tune("RT_SPLIT_MIN", m)
             img, st = sc.render(cam, seed=9, rank=0, nranks=nranks, chunk=K)
             assert np.array_equal(img, ref, equal_nan=True), (m, K)
             assert st["segments"] == st0["segments"], (m, K)
 
 
-def test_big_spheres_outside_the_bvh_same_image(rt, gpu, monkeypatch):
+def test_big_spheres_outside_the_bvh_same_image(rt, gpu, tune):
     """Spheres of radius >= kBigSphereR are tested before the BVH (trav_init) instead of as
     BVH leaves: the same fp64 test on the same record, so the same closest hits.  book1's
-    ground sphere both ways (RT_BIG_SPHERE_R is read when the scene is created)."""
+    ground sphere both ways (RT_BIG_SPHERE_R is read when the scene is created).
+
+    Not bitwise in general: a hit is accepted when its fp64 root is below the fp32 closest
+    t so far, so two roots within one fp32 ulp of each other are a tie that the TEST ORDER
+    decides, and the order changes when the ground leaves the BVH.  Such ties are not rare
+    here: book1's small spheres rest on the ground, tangent to it, and around every contact
+    point the two surfaces stay within an ulp of each other over a ring ~1e-3 wide.  The
+    differing samples are those ties only, so they are counted and bounded, not hidden
+    behind a tolerance: per-pixel differences stay at one sample's worth."""
     imgs = []
     for r in ("256", "1e30"):
-        monkeypatch.setenv("RT_BIG_SPHERE_R", r)
+        tune("RT_BIG_SPHERE_R", r)
         t, cam, w, l = _scene(rt, "book1", 64, 16)
         with rt.Scene(t, w, l) as sc:
             imgs.append(sc.render(cam, seed=8)[0])
-    m = compare(imgs[0], imgs[1])
-    assert m["frac_close"] >= 0.9999 and m["q_equal"] >= 0.9999, m
+    differ = np.any(imgs[0] != imgs[1], axis=2)
+    ss = cam.derived().spp_sqrt ** 2
+    # a tie moves at most a few of a pixel's ss samples: |delta| <= (samples moved) x (the
+    # largest per-sample channel: the sun's emission 5, main.go:85-87) / ss
+    dmax = float(np.abs(imgs[0].astype(np.float64) - imgs[1]).max())
+    print("big-sphere ties: pixels", int(differ.sum()), "of", differ.size, "max |d|", dmax)
+    assert differ.mean() <= 0.01, differ.sum()
+    assert dmax <= 3 * 5.0 / ss, dmax
 
 
 @pytest.mark.parametrize("name,width,spp", [("cornell", 200, 256), ("book2", 96, 256)])
@@ -197,7 +211,7 @@ def test_kernel_selection(rt, gpu, name, width, lean, width_tree, lds):
 
 @pytest.mark.parametrize("var", ["RT_BRUTE_AXIS", "RT_BRUTE_VERT"])
 @pytest.mark.parametrize("name", ["cornell", "cornell_smoke"])
-def test_axis_record_groups_match_general_test(rt, gpu, monkeypatch, var, name):
+def test_axis_record_groups_match_general_test(rt, gpu, tune, var, name):
     """The record loop's axis-aligned groups (rt_path.h brute_axis) and its y-parallel
     group (brute_vert: the rotated boxes' sides) compute the general quad test's t,
     alpha and beta bit for bit: the Cornell boxes render the same image with either
@@ -205,10 +219,10 @@ def test_axis_record_groups_match_general_test(rt, gpu, monkeypatch, var, name):
     in the loop here (RT_BRUTE_BOX=0): the slab test is checked below."""
     t, cam, w, l = rt.demo_scene(name)
     cam.Width, cam.SamplesPerPixel = 96, 64
-    monkeypatch.setenv("RT_BRUTE_BOX", "0")
+    tune("RT_BRUTE_BOX", "0")
     imgs = []
     for flag in ("0", "1"):
-        monkeypatch.setenv(var, flag)
+        tune(var, flag)
         with rt.Scene(t, w, l) as sc:
             img, st = sc.render(cam, seed=4)
         assert st["tree_width"] == 0
@@ -217,7 +231,7 @@ def test_axis_record_groups_match_general_test(rt, gpu, monkeypatch, var, name):
 
 
 @pytest.mark.parametrize("name", ["cornell", "cornell_smoke"])
-def test_record_loop_boxes(rt, oracle, gpu, monkeypatch, name):
+def test_record_loop_boxes(rt, oracle, gpu, tune, name):
     """Boxes rotated about y are tested as one slab test each in the record loop
     (rt_path.h brute_box, the reference's rotateY frame): Cornell's two boxes are found,
     the smoke scene's boxes are media boundaries (not records), and the image agrees
@@ -227,7 +241,7 @@ def test_record_loop_boxes(rt, oracle, gpu, monkeypatch, name):
     ref, _ = oracle.render(t, w, l, cam, seed=4, threads=8)
     ms, boxes = [], []
     for flag in ("0", "1"):
-        monkeypatch.setenv("RT_BRUTE_BOX", flag)
+        tune("RT_BRUTE_BOX", flag)
         with rt.Scene(t, w, l) as sc:
             img, st = sc.render(cam, seed=4)
         assert st["tree_width"] == 0
@@ -389,7 +403,7 @@ def test_maxcontribution_clamp_on_gpu(rt, gpu):
 
 
 @pytest.mark.parametrize("name", ["book2", "book1"])
-def test_image_independent_of_schedule_knobs(rt, gpu, name, monkeypatch):
+def test_image_independent_of_schedule_knobs(rt, gpu, name, tune):
     """The chunk order (row groups), the traversal step budget, the ready-lane count
     before shading and the chunk batch size only change WHEN work runs, never what a
     sample computes: with exact pixel sums the image is bit-identical under every
@@ -400,7 +414,7 @@ def test_image_independent_of_schedule_knobs(rt, gpu, name, monkeypatch):
         for var, val in (("RT_CHUNK_ROWS", "1"), ("RT_CHUNK_ROWS", "100000"),
                          ("RT_STEP_BUDGET", "3"), ("RT_STEP_BUDGET", "1000000"),
                          ("RT_SHADE_MIN", "40"), ("RT_GRAB_MIN", "1")):
-            monkeypatch.setenv(var, val)
+            tune(var, val)
             img, _ = sc.render(cam, seed=6)
-            monkeypatch.delenv(var)
+            tune(var, None)
             assert np.array_equal(base, img, equal_nan=True), (var, val)

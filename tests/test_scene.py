@@ -134,19 +134,19 @@ def bvh8_invariants(sc):
 
 
 @pytest.mark.parametrize("name", ["book2", "model:96x24"])
-def test_bvh8_invariants(rt, name, monkeypatch):
-    monkeypatch.setenv("RT_BVH8", "1")  # the wide tree is opt-in
+def test_bvh8_invariants(rt, name, tune):
+    tune("RT_BVH8", "1")  # the wide tree is opt-in
     t, cam, w, l = rt.demo_scene(name)
     with rt.Scene(t, w, l) as sc:
         nodes, _ = bvh8_invariants(sc)
     assert len(nodes) >= 2
 
 
-def test_bvh8_only_when_asked_and_large(rt, monkeypatch):
+def test_bvh8_only_when_asked_and_large(rt, tune):
     t, cam, w, l = rt.demo_scene("book2")
     with rt.Scene(t, w, l) as sc:  # default: no BVH8
         assert len(sc.export_bvh8()[0]) == 0
-    monkeypatch.setenv("RT_BVH8", "1")
+    tune("RT_BVH8", "1")
     t, cam, w, l = rt.demo_scene("book1")  # 485 prims: the BVH4 (LDS-sized scenes)
     with rt.Scene(t, w, l) as sc:
         assert len(sc.export_bvh8()[0]) == 0
@@ -203,13 +203,13 @@ def test_demo_scene_numbers(rt):
     assert rt.lib().rt_demo_scene_name(9, C.byref(name)) < 0
 
 
-def test_bvh_build_is_thread_count_invariant(rt, monkeypatch):
+def test_bvh_build_is_thread_count_invariant(rt, tune):
     """The SAH build runs its top levels with threaded loops and the subtrees in
     parallel (host_bvh.cpp); min/max box growth and integer bin counts make the
     tree bit-identical for any thread count."""
     out = {}
     for th in ("1", "3", "8"):
-        monkeypatch.setenv("RT_THREADS", th)
+        tune("RT_THREADS", th)
         t, cam, w, l = rt.demo_scene("model:256x64")
         with rt.Scene(t, w, l) as sc:
             nodes, refs, root, bounds = sc.export_bvh()
@@ -217,7 +217,7 @@ def test_bvh_build_is_thread_count_invariant(rt, monkeypatch):
     assert out["1"] == out["3"] == out["8"]
 
 
-def test_box_leaves_kept_only_where_they_pay(rt, monkeypatch):
+def test_box_leaves_kept_only_where_they_pay(rt, tune):
     """NewBox becomes one BVH leaf (rt_device.h "box leaf") in large scenes whose kernel
     set has FT_BOX; small scenes and lean sets keep the six quads, so their trees and
     images are exactly the per-quad ones."""
@@ -229,12 +229,12 @@ def test_box_leaves_kept_only_where_they_pay(rt, monkeypatch):
         i = sc.info()
         bvh_invariants(sc)
     assert i["features"] & rt.RT_FT_BOX and i["n_world_prims"] == 64 + 3 + 1 + 1
-    monkeypatch.setenv("RT_BOX_LEAVES", "0")
+    tune("RT_BOX_LEAVES", "0")
     with rt.Scene(t, w, l) as sc:
         j = sc.info()
     assert not j["features"] & rt.RT_FT_BOX and j["n_world_prims"] == 6 * 64 + 3 + 1 + 1
     assert j["n_quads"] == i["n_quads"]  # the same quads either way
-    monkeypatch.delenv("RT_BOX_LEAVES")
+    tune("RT_BOX_LEAVES", None)
     for name in ("cornell", "quads"):  # small: no box leaves
         assert not info(rt, name)["features"] & rt.RT_FT_BOX
     t, cam, w, l = scenes.boxes(rt)  # 216 quads, lean set: expanded

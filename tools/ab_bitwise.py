@@ -18,6 +18,7 @@ SCENES = [("cornell", 64, 64), ("book1", 48, 16), ("book2", 48, 16), ("quads", 3
 def render_all(out):
     sys.path.insert(0, REPO)
     import go_raytracer_amd as rt
+    rt.tune_from_env()  # dev tool: RT_* knobs from the environment (rt_tune_set)
     res = {}
     for name, w, spp in SCENES:
         t, cam, wo, li = rt.demo_scene(name)

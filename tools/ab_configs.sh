@@ -1,4 +1,5 @@
 #!/bin/bash
+set -o pipefail  # a failed GPU step in a pipeline ends the script with its own status
 # A/B the in-tree library against go_raytracer_amd/build_prev on the full-size
 # configs, alternating, in one box (dev tool): tools/ab_configs.sh OUTLOG
 OUT=$1

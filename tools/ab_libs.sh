@@ -1,4 +1,5 @@
 #!/bin/bash
+set -o pipefail  # a failed GPU step in a pipeline ends the script with its own status
 # Time named library builds on several configs, alternating (dev tool):
 #   tools/ab_libs.sh OUTLOG REPS "name=path.so,name2=path2.so,..." "scene width spp" ...
 # "cur" (or an empty path) is the in-tree library.  One JSON line per render

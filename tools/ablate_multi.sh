@@ -1,4 +1,5 @@
 #!/bin/bash
+set -o pipefail  # a failed GPU step in a pipeline ends the script with its own status
 # Time library builds on several configs, alternating (dev tool):
 #   tools/ablate_multi.sh OUTLOG REPS "scene width spp" ...
 # Libraries: the in-tree one ("cur"), go_raytracer_amd/build_prev ("prev", if built by

@@ -8,10 +8,11 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import go_raytracer_amd as rt  # noqa: E402
+rt.tune_from_env()  # dev tool: RT_* knobs from the environment (rt_tune_set)
 
 W, SPP = int(sys.argv[1]), int(sys.argv[2])
 for flag in ("0", "1"):
-    os.environ["RT_BRUTE_BOX"] = flag
+    rt.tune("RT_BRUTE_BOX", flag)
     t, cam, w, l = rt.demo_scene("cornell")
     cam.Width, cam.SamplesPerPixel = W, SPP
     with rt.Scene(t, w, l) as sc:

@@ -3,6 +3,7 @@
 import json, os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import go_raytracer_amd as rt
+rt.tune_from_env()  # dev tool: RT_* knobs from the environment (rt_tune_set)
 
 for nbox in [int(x) for x in sys.argv[1].split(",")]:
     t, cam, w, l = rt.demo_scene("cornell")
@@ -20,8 +21,9 @@ for nbox in [int(x) for x in sys.argv[1].split(",")]:
                    "smem": {"RT_BRUTE_MAX": "100000", "RT_BRUTE_SMEM": "1"},
                    "2": {"RT_TREE": "2", "RT_BRUTE_MAX": "0", "RT_BRUTE_SMEM": "0"},
                    "4": {"RT_TREE": "4", "RT_BRUTE_MAX": "0", "RT_BRUTE_SMEM": "0"}}[mode]
-            os.environ.pop("RT_TREE", None)
-            os.environ.update(env)
+            rt.untune("RT_TREE")
+            for k, v in env.items():
+                rt.tune(k, v)
             sc.render(cam, seed=1, mode="fused")
             t0 = time.time()
             img, st = sc.render(cam, seed=1, mode="fused")

@@ -1,4 +1,5 @@
 #!/bin/bash
+set -o pipefail  # a failed GPU step in a pipeline ends the script with its own status
 # Build the library of git revision REV (default HEAD) into go_raytracer_amd/build_prev (A/B baseline).
 REV=${1:-HEAD}
 set -e

@@ -1,4 +1,5 @@
 #!/bin/bash
+set -o pipefail  # a failed GPU step in a pipeline ends the script with its own status
 # Build the working tree's library with extra hipcc flags into
 # go_raytracer_amd/build_abl/NAME/librt_amd.so (dev tool, A/B variants):
 #   tools/build_variant.sh NAME "-DMESH_WLDS=2 -DMESH_SHORT=12"

@@ -3,6 +3,7 @@ usage chunk_probe.py scene width spp [nranks]"""
 import json, os, sys
 sys.path.insert(0, os.getcwd())
 import go_raytracer_amd as rt
+rt.tune_from_env()  # dev tool: RT_* knobs from the environment (rt_tune_set)
 scene, width, spp = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
 n = int(sys.argv[4]) if len(sys.argv) > 4 else 1
 t, cam, w, l = rt.demo_scene(scene)

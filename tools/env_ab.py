@@ -11,6 +11,7 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import go_raytracer_amd as rt  # noqa: E402
+rt.tune_from_env()  # dev tool: RT_* knobs from the environment (rt_tune_set)
 
 var, out_path, specs = sys.argv[1], sys.argv[2], sys.argv[3:]
 vals = (0, 1)
@@ -20,7 +21,7 @@ if "=" in var:
 
 
 def render(scene, width, spp, val, seed=3):
-    os.environ[var] = str(val)
+    rt.tune(var, val)
     t, cam, w, l = rt.demo_scene(scene)
     cam.Width = width
     with rt.Scene(t, w, l) as sc:

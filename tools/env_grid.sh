@@ -1,4 +1,5 @@
 #!/bin/bash
+set -o pipefail  # a failed GPU step in a pipeline ends the script with its own status
 # Library switches read at render time, on the share probe (dev tool):
 #   tools/env_grid.sh OUT "scene width spp" "VAR=val[,VAR2=val2]" ...   ("-": no switch)
 # e.g. "RT_TAIL_FRAC=4,RT_TAIL_K=2" or "RT_SPLIT_MIN=2".  One JSON line per share

@@ -3,6 +3,7 @@ usage: gpu_probe.py scene width spp [modes] [aspect]"""
 import sys, time, json
 sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 import go_raytracer_amd as rt
+rt.tune_from_env()  # dev tool: RT_* knobs from the environment (rt_tune_set)
 
 scene = sys.argv[1] if len(sys.argv) > 1 else "cornell"
 width = int(sys.argv[2]) if len(sys.argv) > 2 else 800

@@ -1,4 +1,5 @@
 #!/bin/bash
+set -o pipefail  # a failed GPU step in a pipeline ends the script with its own status
 # Client-side wrapper (dev tool): run one gpurun call, and call again only when gpurun
 # reports that no box was taken (exit 3: no free box, or an infrastructure failure before
 # the command ran; nothing ran and nothing was charged).  Any other exit status, including

@@ -1,4 +1,5 @@
 # A/B of the SAH leaf size (dev tool): RT_BVH_LEAF 1 | 2 | 4 on C3/C4 shapes
+set -o pipefail  # a failed GPU step in a pipeline ends the script with its own status
 for rep in 1 2; do
 for lf in 1 2 4; do
   export RT_BVH_LEAF=$lf

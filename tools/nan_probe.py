@@ -8,6 +8,7 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import go_raytracer_amd as rt  # noqa: E402
+rt.tune_from_env()  # dev tool: RT_* knobs from the environment (rt_tune_set)
 
 np.set_printoptions(linewidth=220, precision=7, suppress=False)
 W, SPP, PIX, S = (int(a) for a in sys.argv[1:5])

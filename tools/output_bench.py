@@ -17,6 +17,8 @@ import torch  # noqa: E402
 
 import go_raytracer_amd as rt  # noqa: E402
 
+rt.tune_from_env()  # dev tool: RT_* knobs from the environment (rt_tune_set)
+
 
 def best(fn, reps=10):
     ts = []

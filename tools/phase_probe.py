@@ -13,6 +13,7 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import go_raytracer_amd as rt  # noqa: E402
+rt.tune_from_env()  # dev tool: RT_* knobs from the environment (rt_tune_set)
 
 NAMES = ["grab", "trav", "media", "shade", "tex", "light", "term", "loop",
          "trav_lanes", "trav_rounds", "shade_lanes", "shade_rounds", "step_lanes", "step_wave"]
@@ -26,10 +27,10 @@ with rt.Scene(t, w, l) as sc:
     cam.SamplesPerPixel = 1
     sc.render(cam)
     cam.SamplesPerPixel = spp
-    os.environ["RT_WAVE_TIMES"] = path
+    rt.tune("RT_WAVE_TIMES", path)
     kw = {"chunk": int(os.environ["CHUNK"])} if "CHUNK" in os.environ else {}
     img, st = sc.render(cam, profile=True, nranks=int(os.environ.get("NRANKS", "1")), **kw)
-    os.environ.pop("RT_WAVE_TIMES")
+    rt.untune("RT_WAVE_TIMES")
 a = np.fromfile(path, dtype=np.uint64).reshape(-1, 18).astype(np.float64)
 ph = a[:, 4:].sum(axis=0)
 loop = ph[7]

@@ -122,6 +122,7 @@ def collect(tag, cfg):
 def main():
     sys.path.insert(0, REPO)
     import go_raytracer_amd as rt
+    rt.tune_from_env()  # dev tool: RT_* knobs from the environment (rt_tune_set)
     tag, cfgs = sys.argv[1], sys.argv[2:] or list(CONFIGS)
     try:
         with open(os.path.join(REPO, "profiles", "traffic.json")) as f:

@@ -1,4 +1,5 @@
 # Fused-loop scheduling sweep (dev tool): RT_STEP_BUDGET x RT_SHADE_MIN on C3-C5 shapes
+set -o pipefail  # a failed GPU step in a pipeline ends the script with its own status
 run() {  # scene width spp budget shade_min
   RT_STEP_BUDGET=$4 RT_SHADE_MIN=$5 timeout -k 10 200 python3 tools/gpu_probe.py $1 $2 $3 fused |
     sed "s/^{/{\"step_budget\": $4, \"shade_min\": $5, /"

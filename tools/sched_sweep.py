@@ -3,6 +3,7 @@ python3 tools/sched_sweep.py scene width spp  budget1,budget2 shade1,shade2"""
 import json, os, sys, time
 sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 import go_raytracer_amd as rt
+rt.tune_from_env()  # dev tool: RT_* knobs from the environment (rt_tune_set)
 
 scene, width, spp = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
 budgets = [int(x) for x in sys.argv[4].split(",")]
@@ -15,7 +16,7 @@ with rt.Scene(t, w, l) as sc:
     sc.render(cam, seed=1, mode="fused")
     for b in budgets:
         for m in shades:
-            os.environ["RT_STEP_BUDGET"], os.environ["RT_SHADE_MIN"] = str(b), str(m)
+            rt.tune("RT_STEP_BUDGET", b), rt.tune("RT_SHADE_MIN", m)
             t0 = time.time()
             img, st = sc.render(cam, seed=1, mode="fused")
             dt = time.time() - t0

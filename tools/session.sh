@@ -1,4 +1,5 @@
 #!/bin/bash
+set -o pipefail  # a failed GPU step in a pipeline ends the script with its own status
 # One GPU session from a list of steps (dev tool): tools/session.sh TAG 'cmd1' 'cmd2' ...
 # Each step runs under its own time limit (prefix it with `timeout -k 10 N`), its stdout and
 # stderr go to gpurun_out/TAG_<i>.log.  Exit status 1 (a failed assertion, a non-zero

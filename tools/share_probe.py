@@ -13,6 +13,8 @@ import torch  # noqa: E402
 
 import go_raytracer_amd as rt  # noqa: E402
 
+rt.tune_from_env()  # dev tool: RT_* knobs from the environment (rt_tune_set)
+
 scene = sys.argv[1] if len(sys.argv) > 1 else "cornell"
 width = int(sys.argv[2]) if len(sys.argv) > 2 else 800
 spp = int(sys.argv[3]) if len(sys.argv) > 3 else 1024

@@ -3,6 +3,7 @@ row shares (dev tool): usage slots_probe.py scene width spp"""
 import json, os, sys
 sys.path.insert(0, os.getcwd())
 import go_raytracer_amd as rt
+rt.tune_from_env()  # dev tool: RT_* knobs from the environment (rt_tune_set)
 scene, width, spp = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
 t, cam, w, l = rt.demo_scene(scene)
 cam.Width, cam.SamplesPerPixel = width, spp

@@ -3,6 +3,7 @@ import sys
 sys.path.insert(0, ".")
 import numpy as np
 import go_raytracer_amd as rt
+rt.tune_from_env()  # dev tool: RT_* knobs from the environment (rt_tune_set)
 from oracle import pyoracle
 from tests import scenes
 

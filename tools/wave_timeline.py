@@ -10,6 +10,7 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import go_raytracer_amd as rt  # noqa: E402
+rt.tune_from_env()  # dev tool: RT_* knobs from the environment (rt_tune_set)
 
 t, cam, w, l = rt.demo_scene("cornell")
 cam.Width, cam.SamplesPerPixel = 800, 1024
@@ -17,9 +18,9 @@ path = "/tmp/wave_times.bin"
 with rt.Scene(t, w, l) as sc:
     for n in [int(x) for x in sys.argv[1:]] or [1, 8]:
         sc.render(cam, nranks=n)
-        os.environ["RT_WAVE_TIMES"] = path
+        rt.tune("RT_WAVE_TIMES", path)
         img, st = sc.render(cam, nranks=n, profile=True)
-        os.environ.pop("RT_WAVE_TIMES")
+        rt.untune("RT_WAVE_TIMES")
         a = np.fromfile(path, dtype=np.uint64).reshape(-1, 18).astype(np.int64)
         t0 = a[:, 0].min()
         start = (a[:, 0] - t0) / 100.0  # 100 MHz -> µs
