@@ -144,7 +144,11 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
   const bool recs_lds = LDS && TREE != 8 && stage_nodes(P, lnodes, TREE == 4 ? 8 : 4);
   if (!LDS) __syncthreads();  // staged tables visible to every wave (stage_nodes ends with one)
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;  // weight-stack column
-  const TravStack ts = {&lstack[threadIdx.x], P.ostack + slot, P.stack_cols, fused_short(FT, TREE)};
+  const TravStack ts = {&lstack[threadIdx.x], P.ostack + slot, P.stack_cols, fused_short(FT, TREE)
+#ifdef RT_COUNT_TRAV_OVF
+                        , &P.ctr->pushes
+#endif
+  };
   const WStack ws = {&lw[threadIdx.x], fused_wlds(FT, TREE)};
   const SampleAcc sa = {&lacc[threadIdx.x]};
   Path s;

@@ -393,9 +393,18 @@ struct TravStack {
   uint32_t* ovf;     // &ostack[slot], stride cols
   uint32_t cols;
   int nshort;        // LDS entries (a compile-time constant of each kernel)
+#ifdef RT_COUNT_TRAV_OVF
+  unsigned long long* dbg;  // debug builds: HBM overflow pushes, into Counters::pushes
+#endif
   RT_D void push(int sp, uint32_t v) const {
-    if (sp < nshort) ((lds_u32*)lds)[sp * 256] = v;
-    else ((glb_u32*)ovf)[(size_t)(sp - nshort) * cols] = v;
+    if (sp < nshort) {
+      ((lds_u32*)lds)[sp * 256] = v;
+    } else {
+      ((glb_u32*)ovf)[(size_t)(sp - nshort) * cols] = v;
+#ifdef RT_COUNT_TRAV_OVF
+      if (dbg) atomicAdd(dbg, 1ull);
+#endif
+    }
   }
   RT_D uint32_t pop(int sp) const {
     uint32_t v;
@@ -1747,6 +1756,17 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
   // shade table in LDS (rt_render.hip), no global loads
   bool ltab = false;
   f3 lcol = mk3(0, 0, 0);
+  // The hit point goes back onto the surface it was found on.  r.At(t) in fp32 carries
+  // the rounding of t along the ray (~|p - o| * 2^-22: up to ~1e-4 off the surface for the
+  // long rays of the 555- and 1000-unit scenes), and from a point that far on the wrong
+  // side a next ray leaving at a grazing angle re-hits the same quad or sphere at t >=
+  // 0.001 -- a vertex the fp64 reference (point on the surface to ~1e-13) never makes.
+  // That self-hit was 98 % of C2's and ~40 % of C4's forked samples
+  // (tools/fork_census.py).  Quads: projected onto their plane, p - n (n.p - D), exact for
+  // axis-aligned quads (every term is an exact zero or a Sterbenz difference, so p lands
+  // ON the plane and the next test's t is exactly 0).  Spheres: onto the sphere, and then
+  // `eta` (4x the rounding left) to the side the next ray leaves on (below).
+  float eta = 0.0f;
   if (ref != PRIM_NONE) {
     const float t = h.t;
     p = o + d * t;  // r.At(t)
@@ -1756,7 +1776,26 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
     if (HAS(FT_SPHERE) && type == PRIM_SPHERE) {
       const F4 cr = sc.sph_cr[idx], mv = sc.sph_mv[idx];
       f3 cc = xyz(cr) + xyz(mv) * time;
-      nout = (p - cc) * rcp(cr.w);
+      // p moved along the unit normal by r - |p - c|, that offset from r^2 - |p - c|^2
+      // formed in fp64 (the sphere test's centre; every fp32 square is exact there), so the
+      // point is on the sphere to its coordinates' rounding, ~2^-24 sum|p_i n_i|, even for
+      // the R=1000 ground where p - c cancels in fp32.  eta, 4x that bound, then puts it
+      // on the right side (below).  nout = (p - c) / r objects.go:102 (a negative radius
+      // keeps its inward normal).
+      {
+        const double cx = (double)cr.x + (double)time * (double)mv.x;
+        const double cy = (double)cr.y + (double)time * (double)mv.y;
+        const double cz = (double)cr.z + (double)time * (double)mv.z;
+        const double ex = (double)p.x - cx, ey = (double)p.y - cy, ez = (double)p.z - cz;
+        const double rr = (double)cr.w;
+        const float dn = (float)(rr * rr - (ex * ex + ey * ey + ez * ez));  // (r - |e|)(r + |e|)
+        const f3 e = p - cc;
+        const float le = length(e);
+        const f3 nu = e * rcp(le);
+        p = p + nu * (dn * rcp(fabsf(cr.w) + le));
+        nout = cr.w < 0.0f ? -nu : nu;
+        eta = 0x1p-22f * (fabsf(p.x * nu.x) + fabsf(p.y * nu.y) + fabsf(p.z * nu.z));
+      }
       mat = (int)fbits(mv.w);
       ff = dot(d, nout) < 0;  // setFaceNormal hittable.go:27-34
       n = ff ? nout : -nout;
@@ -1770,9 +1809,12 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
       }
     } else if (FT == 0u && sc.shade_lds >= 0) {
       const F4* tab = g_dyn_lds + sc.shade_lds + 2 * idx;
-      const F4 a = ld_lds(tab);
-      lcol = xyz(ld_lds(tab + 1));
+      const F4 a = ld_lds(tab), b = ld_lds(tab + 1);
+      lcol = xyz(b);
       nout = xyz(a);
+#ifndef RT_NO_LEAN_SNAP  // (A/B builds: the record-loop kernel without the projection)
+      p = p - nout * (dot(nout, p) - b.w);  // onto the plane n.p = D (b.w, rt_render.hip)
+#endif
       mat = (int)fbits(a.w);  // the material KIND here
       ltab = true;
       ff = dot(d, nout) < 0;
@@ -1780,6 +1822,7 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
     } else if (!HAS(FT_TRI | FT_MEDIA) || type == PRIM_QUAD) {
       const F4* q = sc.quad + 5 * (size_t)idx;
       nout = xyz(q[3]);
+      p = p - nout * (dot(nout, p) - q[0].w);  // onto the plane n.p = D
       mat = (int)fbits(q[2].w);
       ff = dot(d, nout) < 0;
       n = ff ? nout : -nout;
@@ -1969,6 +2012,11 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
         term = true;
         lterm = mk3(0, 0, 0);
       } else {
+        // spheres: the new origin eta off the surface on the side the ray leaves to, so
+        // the fp64 sphere test (exact for this fp32 point) sees it where the reference's
+        // point is: outside for a ray leaving outward (no root ahead), inside for one
+        // refracted or fuzz-reflected inward (the far root only).  eta = 0 elsewhere.
+        if (HAS(FT_SPHERE)) p = p + n * copysignf(eta, dot(ndir, n));
         s.o = p;
         s.d = ndir;
         s.spare = rt_spare24(r);

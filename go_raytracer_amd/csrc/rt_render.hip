@@ -727,7 +727,9 @@ static int upload_scene(const Scene* s, DeviceScene* ds) {
         const uint32_t kind = (uint32_t)m.kind;
         memcpy(&kb, &kind, 4);
         tab[2 * qi] = {q[3].x, q[3].y, q[3].z, kb};
-        tab[2 * qi + 1] = h.texs[m.tex].color;
+        // the colour, and the plane offset D (shade_core puts the hit point on the plane)
+        const F4 col = h.texs[m.tex].color;
+        tab[2 * qi + 1] = {col.x, col.y, col.z, q[0].w};
       }
       ds->shade_n = ok && env_int("RT_SHADE_LDS", 1) != 0 ? (int32_t)tab.size() : 0;
       if (ds->shade_n) pairs.insert(pairs.end(), tab.begin(), tab.end());
