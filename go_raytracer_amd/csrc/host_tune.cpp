@@ -45,6 +45,7 @@ constexpr Knob kKnobs[] = {
     // every render (rt_render.hip render_impl)
     {"RT_TREE", true},             // 2 / 4: force the BVH2 / BVH4 over the record loop
     {"RT_BRUTE_SMEM", false},      // 1: record loop through the scalar cache
+    {"RT_QBVH", false},            // 0: 128-B BVH4 nodes instead of the compressed 64-B ones
     {"RT_CHUNK_NEED", false},      // chunks per lane that pick the chunk size
     {"RT_TAIL_FRAC", false},       // tail phase: 1 / fraction of the samples
     {"RT_TAIL_K", false},          // tail phase chunk size

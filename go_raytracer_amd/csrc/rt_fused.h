@@ -131,7 +131,8 @@ constexpr unsigned fused_static_lds(uint32_t ft, int tree = 4) {
   return (unsigned)(fused_short(ft, tree) * 4 + fused_wlds(ft, tree) * 12 + 24) * 256u +
          ((ft & FT_NOISE) ? 256u * 16u + 768u : 0u);
 }
-// TREE: 4 = BVH4, 2 = BVH2, 0 = no tree (every record tested, tiny scenes)
+// TREE: 4 = BVH4, 5 = compressed BVH4 (64-B nodes, global only), 2 = BVH2, 0 = no tree
+// (every record tested, tiny scenes)
 template <bool LDS, uint32_t FT, int TREE>
 __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) {
   extern __shared__ F4 lnodes[];  // LDS scene cache, sized at launch (scene_lds_bytes)
@@ -210,8 +211,9 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
       }
       else
       {
-        const int nsteps = trav_steps<LDS, FT, TREE == 4>(P.sc, lnodes, recs_lds, ts, s.o, s.d,
-                                                          s.time, 0.001f, tr, P.step_budget);
+        // TREE 5: the compressed BVH4 (64-B items, host_qbvh.cpp), read through L1/L2
+        const int nsteps = trav_steps<LDS, FT, TREE == 4 || TREE == 5, TREE == 5>(
+            P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, tr, P.step_budget);
 #ifdef RT_PHASES
         ph_steps(nsteps);
 #endif
@@ -279,6 +281,8 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
   X(true, (FT_SPHERE | FT_TRI | FT_METAL), 4)                               \
   X(false, (FT_SPHERE | FT_TRI | FT_METAL), 4)                              \
   X(true, (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER), 4)        \
-  X(false, (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER), 4)
+  X(false, (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER), 4)       \
+  X(false, (FT_SPHERE | FT_TRI | FT_METAL), 5)                              \
+  X(false, (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER), 5)
 
 }  // namespace rt

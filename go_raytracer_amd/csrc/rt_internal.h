@@ -140,6 +140,10 @@ int build_bvh(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi
 // host_bvh8.cpp: the BVH8 of s.nodes (the binary tree) -> s.nodes8 / s.refs8
 constexpr size_t kBvh8MinRefs = 1024;
 int build_bvh8(HostScene& s);
+// host_qbvh.cpp: s's BVH4 as 64-B compressed nodes with the single-prim leaf records inline
+// (rt_device.h "compressed BVH4 node"); *n_items = 0 when the tree is not encodable
+int build_qbvh(const HostScene& s, const std::vector<F4>& recs, std::vector<F4>* out,
+               size_t* n_items);
 // rt_build.hip: the same outputs as build_bvh, built by PLOC on `device` (-1: the calling
 // thread's current device; the current device is restored on return)
 int build_bvh_device(HostScene& s, const std::vector<F4>& lo, const std::vector<F4>& hi,

@@ -457,7 +457,13 @@ RT_D void trav_init(const DevScene& sc, f3 o, f3 d, float time, Trav& tr) {
 
 // LDS instantiation: lnodes holds the node array and, when recs_lds, the leaf
 // records right after it (uniform flag: both load forms exist, one runs)
-template <bool LDS, uint32_t FT, bool W4 = true>
+// one fp16 half of a 32-bit word as fp32 (an fma on it compiles to v_fma_mix_f32)
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+template <int H> RT_D float half_of(uint32_t w) { return (float)__builtin_bit_cast(h2v, w)[H]; }
+
+// QN: the compressed BVH4 (host_qbvh.cpp, rt_device.h "compressed BVH4 node"), 64-B
+// items read through L1/L2; cur = item index, LEAF_BIT set for a single-prim leaf record
+template <bool LDS, uint32_t FT, bool W4 = true, bool QN = false>
 RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const TravStack& stack,
                      f3 o, f3 d, float time, float tmin, Trav& tr, int budget) {
   uint32_t cur = tr.cur;
@@ -479,6 +485,90 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
   const f3 inv = tr.inv;
   int n = 0;
   for (; n < budget && cur != TRAV_DONE; ++n) {
+    if constexpr (QN) {
+      // One 64-B item per step, node or leaf record alike (4 x 16 B, issued together).
+      const bool leaf = (cur & LEAF_BIT) != 0u;
+      const F4* it = (const F4*)((const char*)sc.nodes + ((cur & 0x0FFFFFFFu) << 6));
+      F4 v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = ld_glb(it + e);
+      if (!leaf) {
+        // t = off * inv + (corner - o) * inv per plane (v_fma_mix_f32 on the fp16 offset).
+        // Planes come as (lo 0|1, lo 2|3, hi 0|1, hi 2|3) per axis; the near pair is lo when
+        // inv >= 0 and hi otherwise (a sign-mask select per word), so no min/max per axis.
+        const float bx = (v[0].x - o.x) * inv.x, by = (v[0].y - o.y) * inv.y,
+                    bz = (v[0].z - o.z) * inv.z;
+        const uint32_t info = fbits(v[0].w);
+        const uint32_t base = info & 0x0FFFFFFFu, lmask = info >> 28;
+        const uint32_t mx = neg_mask(inv.x), my = neg_mask(inv.y), mz = neg_mask(inv.z);
+        const uint32_t nx[2] = {pick_by(fbits(v[1].x), fbits(v[1].z), mx), pick_by(fbits(v[1].y), fbits(v[1].w), mx)};
+        const uint32_t fx[2] = {pick_by(fbits(v[1].z), fbits(v[1].x), mx), pick_by(fbits(v[1].w), fbits(v[1].y), mx)};
+        const uint32_t ny[2] = {pick_by(fbits(v[2].x), fbits(v[2].z), my), pick_by(fbits(v[2].y), fbits(v[2].w), my)};
+        const uint32_t fy[2] = {pick_by(fbits(v[2].z), fbits(v[2].x), my), pick_by(fbits(v[2].w), fbits(v[2].y), my)};
+        const uint32_t nz[2] = {pick_by(fbits(v[3].x), fbits(v[3].z), mz), pick_by(fbits(v[3].y), fbits(v[3].w), mz)};
+        const uint32_t fz[2] = {pick_by(fbits(v[3].z), fbits(v[3].x), mz), pick_by(fbits(v[3].w), fbits(v[3].y), mz)};
+        const float tmax = tr.best.t;
+        float tn[4];
+        uint32_t ch[4];
+        auto child = [&](auto hk, int k) {
+          constexpr int H = decltype(hk)::value;
+          const int w = k >> 1;
+          const float tx0 = fmaf(half_of<H>(nx[w]), inv.x, bx), tx1 = fmaf(half_of<H>(fx[w]), inv.x, bx);
+          const float ty0 = fmaf(half_of<H>(ny[w]), inv.y, by), ty1 = fmaf(half_of<H>(fy[w]), inv.y, by);
+          const float tz0 = fmaf(half_of<H>(nz[w]), inv.z, bz), tz1 = fmaf(half_of<H>(fz[w]), inv.z, bz);
+          const float t0 = fmaxf(fmaxf(tx0, ty0), fmaxf(tz0, tmin));
+          const float t1 = fminf(fminf(tx1, ty1), fminf(tz1, tmax));
+          tn[k] = bitsf(pick_by(fbits(t0), 0x7F800000u, neg_mask(t1 * 1.00000024f - t0)));
+          ch[k] = (base + (uint32_t)k) | (((lmask >> k) & 1u) << 31);
+        };
+        child(std::integral_constant<int, 0>{}, 0);
+        child(std::integral_constant<int, 1>{}, 1);
+        child(std::integral_constant<int, 0>{}, 2);
+        child(std::integral_constant<int, 1>{}, 3);
+        auto cx = [&](int a, int b) {  // as the 128-B path's network
+          const uint32_t m = neg_mask(tn[b] - tn[a]);
+          const uint32_t ta = fbits(tn[a]), tb = fbits(tn[b]);
+          const uint32_t ca = ch[a], cb = ch[b];
+          tn[a] = bitsf(pick_by(ta, tb, m));
+          tn[b] = bitsf(pick_by(tb, ta, m));
+          ch[a] = pick_by(ca, cb, m);
+          ch[b] = pick_by(cb, ca, m);
+        };
+        cx(0, 1);
+        cx(2, 3);
+        cx(0, 2);
+        cx(1, 3);
+        cx(1, 2);
+        if (tn[0] != kInf) {
+          if (sp + 3 <= stack.nshort) {
+            lds_u32* q = (lds_u32*)stack.lds;
+            q[sp * 256] = ch[3];
+            sp += tn[3] != kInf;
+            q[sp * 256] = ch[2];
+            sp += tn[2] != kInf;
+            q[sp * 256] = ch[1];
+            sp += tn[1] != kInf;
+          } else {
+            if (tn[3] != kInf && sp < kStack) push(ch[3]);
+            if (tn[2] != kInf && sp < kStack) push(ch[2]);
+            if (tn[1] != kInf && sp < kStack) push(ch[1]);
+          }
+          cur = ch[0];
+          continue;
+        }
+      } else {
+        float t, u, vv;
+        uint32_t ref;
+        const uint32_t rej = hit_record_m<FT>(v, o, d, inv.y, time, tmin, tr.best.t, t, u, vv, ref);
+        tr.best.t = bitsf(pick_by(fbits(t), fbits(tr.best.t), rej));
+        tr.best.u = bitsf(pick_by(fbits(u), fbits(tr.best.u), rej));
+        tr.best.v = bitsf(pick_by(fbits(vv), fbits(tr.best.v), rej));
+        tr.best.ref = pick_by(ref, tr.best.ref, rej);
+      }
+      if (sp == 0) cur = TRAV_DONE;
+      else cur = stack.pop(--sp);
+      continue;
+    }
 #ifndef RT_SPLIT_FETCH
     if (W4 && !LDS) {
       // One fetch per step for node and leaf lanes alike: the node (nodes + 8 cur,
@@ -996,33 +1086,42 @@ template <bool SMEM>
 RT_D uint32_t box_face(const DevScene& sc, const F4* lrec, uint32_t code, f3 o, f3 d, float iy,
                        float best) {
   const uint32_t base = 32u * ((code & ~kBoxCode) >> 2) + ((code >> 1) & 1u);
-  float f[14];
+  float f[8];  // C.x, C.z, a.x, a.z, b.x, b.z, ylo, yhi (then the six face slots)
   if (SMEM) {
     const float* g = (const float*)sc.leafprims + base;
 #pragma unroll
-    for (int e = 0; e < 14; ++e) f[e] = *(const __attribute__((address_space(1))) float*)(g + 2 * e);
+    for (int e = 0; e < 8; ++e) f[e] = *(const __attribute__((address_space(1))) float*)(g + 2 * e);
   } else {
     const lds_f32* l = (const lds_f32*)lrec + base;
 #pragma unroll
-    for (int e = 0; e < 14; ++e) f[e] = l[2 * e];
+    for (int e = 0; e < 8; ++e) f[e] = l[2 * e];
   }
   const float ex = o.x - f[0], ez = o.z - f[1];
   const float lx = fmaf(ez, f[3], ex * f[2]), lz = fmaf(ez, f[5], ex * f[4]);
   const float ix = rcp(fmaf(d.z, f[3], d.x * f[2])), iz = rcp(fmaf(d.z, f[5], d.x * f[4]));
   const float t[6] = {-lx * ix, fmaf(-lx, ix, ix), (f[6] - o.y) * iy, (f[7] - o.y) * iy,
                       -lz * iz, fmaf(-lz, iz, iz)};
-  const bool leave = (code & 1u) != 0u;
-  int face = 0;
+  // Entering plane of slab a: the smaller t (ties: the lo plane); leaving: the larger.  The
+  // face is the first slab whose plane t is nearest the winning t.  As sign-mask selects and
+  // ONE load of the face slot: written with dynamic indices (t[2a + side], f[8 + face]) hipcc
+  // loaded all 14 fields and chained ~60 v_cmp / v_cndmask, about 100 VALU on every shading
+  // round of the record-loop kernel (a wave almost always has a lane whose hit is a box).
+  const uint32_t flip = (code & 1u) ? 0xFFFFFFFFu : 0u;  // leaving: take the larger
+  uint32_t slot = 0u;
   float err = kInf;
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
-    // entering plane of slab a: the smaller t; leaving: the larger
-    const int side = (t[2 * a + 1] < t[2 * a]) != leave ? 1 : 0;
-    const float e = fabsf(t[2 * a + side] - best);
-    face = e < err ? 2 * a + side : face;
-    err = fminf(e, err);
+    const uint32_t m = neg_mask(t[2 * a + 1] - t[2 * a]) ^ flip;  // all ones: the hi plane
+    // (fminf: a NaN distance reads as inf, so it never replaces, as with e < err)
+    const float e = fminf(fabsf(bitsf(pick_by(fbits(t[2 * a]), fbits(t[2 * a + 1]), m)) - best), kInf);
+    const uint32_t nearer = neg_mask(e - err);  // e < err
+    slot = pick_by(slot, 2u * (uint32_t)a + (m & 1u), nearer);
+    err = bitsf(pick_by(fbits(err), fbits(e), nearer));
   }
-  return __float_as_uint(f[8 + face]);
+  if (SMEM)
+    return *(const __attribute__((address_space(1))) uint32_t*)((const float*)sc.leafprims + base +
+                                                                 2 * (8 + slot));
+  return ((const lds_u32*)lrec)[base + 2 * (8 + slot)];
 }
 template <uint32_t FT, bool SMEM>
 RT_D void trav_brute(const DevScene& sc, const F4* lrec, f3 o, f3 d, float time, float tmin,

@@ -202,6 +202,7 @@ struct DeviceScene {
   int32_t brute_boxes = 0;          // boxes among them tested as slabs (rt_path.h brute_box)
   uint32_t root2 = PRIM_NONE;
   int32_t n_nodes2 = 0;
+  const F4* qnodes = nullptr;       // compressed BVH4 (host_qbvh.cpp): 64-B items, root item 0
   ~DeviceScene() {
     for (void* p : allocs) (void)hipFree(p);
   }
@@ -470,6 +471,13 @@ static int upload_scene(const Scene* s, DeviceScene* ds) {
     d.nodes = base;
     d.leafprims = base ? base + rec0 : nullptr;
   }
+  {  // the compressed BVH4 of trees read through L1/L2 (single-prim leaves, render_impl: tree 5)
+    std::vector<F4> qb;
+    size_t items = 0;
+    if ((rc = build_qbvh(h, recs, &qb, &items)) != RT_OK)
+      return rc;
+    if (items && (rc = upload(ds, qb, &ds->qnodes)) != RT_OK) return rc;
+  }
   // the BVH2 and the record-loop pairs serve tiny scenes only (render_impl's tree
   // choice: <= 64 leaf entries); a 1M-triangle scene would upload 64 MB of BVH2
   const size_t tiny = (size_t)std::max(64, env_int("RT_BRUTE_MAX", kBruteMax));
@@ -634,7 +642,14 @@ static int upload_scene(const Scene* s, DeviceScene* ds) {
       const int v = a < 0 ? vert_of(i) : -1;
       grp[a >= 0 ? a : v >= 0 ? 4 + v : 3].push_back(i);
     }
-    for (int a : {0, 1, 2, 4, 5, 6})
+    // An odd axis-aligned group is padded with a record that never hits (D' = NaN: NaN t,
+    // alpha and beta, rejected): two axis pairs cost ~58 VALU, its odd record as a general
+    // pair ~85 (Cornell: the light and the back wall were one general pair).  An odd
+    // axis-parallel group's last record joins the general list.
+    constexpr size_t kAxisPad = (size_t)-3;
+    for (int a : {0, 1, 2})
+      if (grp[a].size() & 1) grp[a].push_back(kAxisPad);
+    for (int a : {4, 5, 6})
       if (grp[a].size() & 1) {
         grp[3].push_back(grp[a].back());  // the group's smallest record
         grp[a].pop_back();
@@ -688,6 +703,10 @@ static int upload_scene(const Scene* s, DeviceScene* ds) {
       }
     }
     for (size_t i = 0; i < slots.size(); ++i) {
+      if (slots[i] == (long)kAxisPad) {  // n = 0, D' = NaN (brute_axis never accepts it)
+        ((float*)&pairs[8 * (i / 2)] + (i & 1))[2 * 3] = NAN;
+        continue;
+      }
       if (slots[i] < 0) continue;
       const F4* r = &recs[4 * (size_t)slots[i]];  // Q|ref, n|D, A, B
       float* f = (float*)&pairs[8 * (i / 2)] + (i & 1);
@@ -867,6 +886,16 @@ static const void* pick_fused(bool lds, uint32_t set, int tree) {
 #endif
     return nullptr;
   }
+  if (tree == 5) {  // the compressed BVH4: trees read through L1/L2
+    if (lds) return nullptr;
+    switch (set) {
+      case kFtSets[2]: return (const void*)k_fused<false, kFtSets[2], 5>;
+      case kFtSets[3]: return (const void*)k_fused<false, kFtSets[3], 5>;
+      case kFtSets[4]: return (const void*)k_fused<false, kFtSets[4], 5>;
+      case FT_ALL: return (const void*)k_fused<false, FT_ALL, 5>;
+      default: return nullptr;
+    }
+  }
   if (tree != 4) return nullptr;  // no such kernel: render_impl never asks (see tree there)
   return lds ? fused_for<true>(set) : fused_for<false>(set);
 }
@@ -976,6 +1005,12 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   if (mode == RT_MODE_FUSED && tree == 4 && !f_lds && !s->h.nodes8.empty() && env_tree != 4 &&
       pick_fused(false, ft_set, 8))
     tree = 8;
+  // Trees read through L1/L2 with single-prim leaves take the compressed BVH4 (64-B nodes,
+  // host_qbvh.cpp): the same closest hits, half the bytes per node step.  RT_QBVH=0: the
+  // 128-B nodes (A/B)
+  if (mode == RT_MODE_FUSED && tree == 4 && !f_lds && ds->qnodes && env_int("RT_QBVH", 1) != 0 &&
+      pick_fused(false, ft_set, 5))
+    tree = 5;
   const void* fused_kernel = pick_fused(f_lds, ft_set, tree);
   if (!fused_kernel) return set_error(RT_ERR_UNSUPPORTED, "internal: no fused kernel for this scene");
   const size_t fused_lds = f_lds ? 64 * (node_slots * n_nodes + (f_recs ? rec_slots : 0)) : 0;
@@ -1113,6 +1148,9 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     p.sc.nodes = ds->nodes2;
     p.sc.root = ds->root2;
     p.sc.n_nodes = ds->n_nodes2;
+  } else if (tree == 5) {
+    p.sc.nodes = ds->qnodes;
+    p.sc.root = 0;  // item 0: the root node (trav_init)
   } else if (tree == 8) {
     p.sc.root = 0;  // BVH8 node 0 (trav_init)
   } else if (tree == 0) {

@@ -377,7 +377,8 @@ typedef struct {
   double ms_fused;       /* fused-kernel time (RT_FLAG_PROFILE) */
   int32_t kernel_features; /* RT_FT_* set compiled into the fused kernel that ran */
   int32_t scene_features;  /* RT_FT_* set the scene needs */
-  int32_t tree_width;      /* BVH arity the kernels traversed (2 or 4) */
+  int32_t tree_width;      /* tree the kernels traversed: 0 none (record loop), 2 BVH2, 4 BVH4,
+                              5 BVH4 with 64-B compressed nodes (large trees) */
   int32_t lds_scene;       /* 1: nodes (and leaf records) ran from the LDS cache */
   int32_t chunk_samples;   /* samples per work chunk (opts.chunk or the adaptive choice) */
   int32_t record_boxes;    /* boxes the record loop tested as one slab test each (0: none) */

@@ -62,7 +62,7 @@ def test_bvh8_renders_like_bvh4(rt, gpu, tune, name, width, spp):
     as the BVH4: the closest hit does not depend on the tree, so the image is the same
     bits (conservative quantisation; ties between coincident surfaces aside).  The BVH8
     kernels are compiled only into A/B builds (-DRT_BVH8_KERNELS): the default
-    library keeps rendering the BVH4, with the same image, when the BVH8 is built."""
+    library keeps rendering the (compressed) BVH4, with the same image, when the BVH8 is built."""
     imgs, widths = [], []
     for v in ("0", "1"):
         tune("RT_BVH8", v)
@@ -72,5 +72,6 @@ def test_bvh8_renders_like_bvh4(rt, gpu, tune, name, width, spp):
             img, st = sc.render(cam, seed=5, mode="fused")
             widths.append(st["tree_width"])
         imgs.append(img)
-    assert widths[0] == 4 and widths[1] in (4, 8), widths
+    # (5: the default library traverses the compressed BVH4 of host_qbvh.cpp)
+    assert widths[0] == 5 and widths[1] in (5, 8), widths
     assert np.array_equal(imgs[0], imgs[1], equal_nan=True)

@@ -195,8 +195,8 @@ def test_full_size_parity_on_row_subsample(rt, oracle, gpu, name, width, spp, as
 # kernel choice (DESIGN.md "Kernels"): the compiled feature set covers the
 # scene's, C2 runs the lean set on its binary tree from LDS, large scenes the BVH4
 @pytest.mark.parametrize("name,width,lean,width_tree,lds", [
-    ("cornell", 64, True, 0, 1), ("book1", 64, False, 4, None), ("book2", 64, False, 4, 0),
-    ("model:256x32", 64, False, 4, 0), ("cornell_smoke", 64, False, 0, 1)])
+    ("cornell", 64, True, 0, 1), ("book1", 64, False, 5, 0), ("book2", 64, False, 5, 0),
+    ("model:256x32", 64, False, 5, 0), ("cornell_smoke", 64, False, 0, 1)])
 def test_kernel_selection(rt, gpu, name, width, lean, width_tree, lds):
     t, cam, w, l = _scene(rt, name, width, 4)
     with rt.Scene(t, w, l) as sc:
@@ -442,3 +442,24 @@ def test_environment_does_not_change_the_image(rt, gpu, name, monkeypatch):
     assert np.array_equal(img, ref, equal_nan=True)
     assert st["segments"] == st0["segments"]
     assert st["tuned"] == 0 and st0["tuned"] == 0
+
+
+@pytest.mark.parametrize("name,width,spp", [("book1", 96, 64), ("book2", 96, 64),
+                                            ("model:256x32", 96, 64), ("model", 160, 16)])
+def test_compressed_bvh_renders_like_bvh4(rt, gpu, tune, name, width, spp):
+    """The compressed BVH4 (host_qbvh.cpp: 64-B nodes, fp16 child planes rounded outwards
+    around an fp32 corner, single-prim leaf records inline) encloses every child box of the
+    128-B BVH4, so its traversal visits a superset of the nodes and finds the same closest
+    hits: the same image bit for bit, and the same segments (RT_QBVH=0 takes the 128-B
+    nodes)."""
+    t, cam, w, l = _scene(rt, name, width, spp)
+    imgs, sts = [], []
+    for q in ("1", "0"):
+        tune("RT_QBVH", q)
+        with rt.Scene(t, w, l) as sc:
+            img, st = sc.render(cam, seed=5)
+        imgs.append(img)
+        sts.append(st)
+    assert [s["tree_width"] for s in sts] == [5, 4]
+    assert np.array_equal(imgs[0], imgs[1], equal_nan=True)
+    assert sts[0]["segments"] == sts[1]["segments"]
