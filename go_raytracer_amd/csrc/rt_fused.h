@@ -131,6 +131,7 @@ constexpr unsigned fused_static_lds(uint32_t ft, int tree = 4) {
   return (unsigned)(fused_short(ft, tree) * 4 + fused_wlds(ft, tree) * 12 + 24) * 256u +
          ((ft & FT_NOISE) ? 256u * 16u + 768u : 0u);
 }
+__shared__ unsigned long long g_tstart[4];  // per wave: k_fused's start time (RT_WAVE_TIMES)
 // TREE: 4 = BVH4, 5 = compressed BVH4 (64-B nodes, global only), 2 = BVH2, 0 = no tree
 // (every record tested, tiny scenes)
 template <bool LDS, uint32_t FT, int TREE>
@@ -167,7 +168,9 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
   tr.cur = TRAV_DONE;
   bool has = false;
   WaveBatch b = batch_init(P);
-  const unsigned long long t_start = P.wave_times ? wall_clock64() : 0ull;
+  // debug (RT_WAVE_TIMES): the wave's start time parks in LDS (a register held across the
+  // loop for this was the record-loop kernel's one spilled VGPR)
+  if (P.wave_times && lane_id() == 0u) g_tstart[threadIdx.x >> 6] = wall_clock64();
   // Scheduling round: lanes without work take a chunk; traversing lanes run up
   // to step_budget traversal steps; lanes whose traversal is done are shaded
   // together once at least shade_min of them wait (or nothing else traverses),
@@ -228,6 +231,7 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
 #ifdef RT_WAVE_SEGS
       wave_segs += n_ready;
 #endif
+
       if (ready) {
         PH_CNT(PH_SHADE_LANES, n_ready);
         PH_CNT(PH_SHADE_ROUNDS, 1);
@@ -260,7 +264,7 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
     if (P.wave_times) {
       const size_t w = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
       unsigned long long* rec = P.wave_times + kWaveRec * w;
-      rec[0] = t_start;
+      rec[0] = g_tstart[threadIdx.x >> 6];
       rec[1] = wall_clock64();
       rec[2] = segs;
       rec[3] = 0ull;

@@ -491,7 +491,15 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
       const F4* it = (const F4*)((const char*)sc.nodes + ((cur & 0x0FFFFFFFu) << 6));
       F4 v[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = ld_glb(it + e);
+      for (int e = 0; e < 3; ++e) v[e] = ld_glb(it + e);
+      // a leaf record's fourth vector is read by quad and box tests only: without quads
+      // in the scene (C5's mesh) a leaf lane fetches 48 B
+#ifdef RT_LEAF64  // (A/B builds: every leaf lane fetches 64 B)
+      v[3] = ld_glb(it + 3);
+#else
+      v[3] = F4{0.0f, 0.0f, 0.0f, 0.0f};
+      if (!leaf || HAS(FT_BOX) || sc.quad != nullptr) v[3] = ld_glb(it + 3);
+#endif
       if (!leaf) {
         // t = off * inv + (corner - o) * inv per plane (v_fma_mix_f32 on the fp16 offset).
         // Planes come as (lo 0|1, lo 2|3, hi 0|1, hi 2|3) per axis; the near pair is lo when
@@ -1127,10 +1135,14 @@ template <uint32_t FT, bool SMEM>
 RT_D void trav_brute(const DevScene& sc, const F4* lrec, f3 o, f3 d, float time, float tmin,
                      Trav& tr) {
   static_assert(!HAS(FT_SPHERE | FT_TRI), "record loop: quad-only feature sets");
-  const int nax = sc.brute_ax[0], nay = sc.brute_ax[1], naz = sc.brute_ax[2];
-  const int nvy = sc.brute_vt[1];  // y-parallel pairs only (RotateY is the only rotation)
+  // the group bounds re-read from the kernel-argument segment on every call (kparams): held
+  // in SGPRs across the kernel's loop they were spilled to VGPR lanes, ~15 v_readlane per
+  // segment in the loops' prologues
+  const cst_params* kp = kparams();
+  const int nax = kp->sc.brute_ax[0], nay = kp->sc.brute_ax[1], naz = kp->sc.brute_ax[2];
+  const int nvy = kp->sc.brute_vt[1];  // y-parallel pairs only (RotateY is the only rotation)
   // general pairs first, then the y-parallel and the axis-aligned groups
-  const int ng = sc.brute_ng;
+  const int ng = kp->sc.brute_ng;
   const v2f ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
   const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z};
   float best = tr.best.t;
@@ -1165,7 +1177,7 @@ RT_D void trav_brute(const DevScene& sc, const F4* lrec, f3 o, f3 d, float time,
   brute_axis<2, SMEM>(sc, lrec, q + nax + nay, q + nax + nay + naz, O, Dv, tmin, best, bk);
   const int qb = q + nax + nay + naz;
   const float iy = rcp(d.y);
-  brute_box<SMEM>(sc, lrec, qb, qb + sc.brute_box, O, Dv, iy, tmin, best, bk);
+  brute_box<SMEM>(sc, lrec, qb, qb + kp->sc.brute_box, O, Dv, iy, tmin, best, bk);
   if (bk != 0xFFFFFFFFu) {
     if (bk & kBoxCode) bk = box_face<SMEM>(sc, lrec, bk, o, d, iy, best);
     // the winner's fields (pair bk/2, half bk&1): Q at floats 8/10/12, A at
@@ -1336,6 +1348,10 @@ RT_D float perlin_noise(PL pl, f3 p) {  // perlin.go:34-54
   const int pi[2] = {pl->perm[0][i & 255], pl->perm[0][(i + 1) & 255]},
             pj[2] = {pl->perm[1][j & 255], pl->perm[1][(j + 1) & 255]},
             pk[2] = {pl->perm[2][k & 255], pl->perm[2][(k + 1) & 255]};
+  // the corner weights i*uu + (1-i)*(1-uu) of perlin.go:49-51 for i = 0, 1: since uu is in
+  // [0, 1], 0*uu + (1-uu) and uu + 0*(1-uu) are exactly 1-uu and uu (hipcc kept the 0*x
+  // terms, which it may not drop for a NaN x: 12 fma per noise call, 84 per turbulence)
+  const float wx[2] = {1 - uu, uu}, wy[2] = {1 - vv, vv}, wz[2] = {1 - ww, ww};
   float accum = 0.0f;
   for (int di = 0; di < 2; ++di)
     for (int dj = 0; dj < 2; ++dj)
@@ -1343,9 +1359,7 @@ RT_D float perlin_noise(PL pl, f3 p) {  // perlin.go:34-54
         const int gi = pi[di] ^ pj[dj] ^ pk[dk];
         const F4 g = {pl->ranvec[gi].x, pl->ranvec[gi].y, pl->ranvec[gi].z, 0.0f};
         f3 wt = mk3(u - (float)di, v - (float)dj, w - (float)dk);
-        accum += ((float)di * uu + (float)(1 - di) * (1 - uu)) *
-                 ((float)dj * vv + (float)(1 - dj) * (1 - vv)) *
-                 ((float)dk * ww + (float)(1 - dk) * (1 - ww)) * dot(xyz(g), wt);
+        accum += wx[di] * wy[dj] * wz[dk] * dot(xyz(g), wt);
       }
   return accum;
 }
@@ -1444,7 +1458,11 @@ RT_D float prim_pdf(const DevScene& sc, uint32_t ref, int li, f3 origin, f3 dir)
     // the light's leaf-record copy (uniform index: scalar loads) and the traversal's quad test
     F4 rec[4];
     if (FT != FT_ALL) {
+#ifdef RT_LIGHTS_SGPR
       const F4* lr = sc.light_recs + 8 * (size_t)__builtin_amdgcn_readfirstlane(li);
+#else
+      const F4* lr = kparams()->sc.light_recs + 8 * (size_t)__builtin_amdgcn_readfirstlane(li);
+#endif
       rec[0] = ld_cst(lr), rec[1] = ld_cst(lr + 1), rec[2] = ld_cst(lr + 2), rec[3] = ld_cst(lr + 3);
     } else {
       const F4* lr = sc.light_recs + 8 * (size_t)li;
@@ -1465,12 +1483,23 @@ RT_D float prim_pdf(const DevScene& sc, uint32_t ref, int li, f3 origin, f3 dir)
 }
 
 // HittableList.PdfValue hittable.go:89-97 over the flattened light table
+// (the light table's size and address re-read from the kernel-argument segment, kparams:
+// held in SGPRs across the fused loop they were spilled to VGPR lanes, one v_readlane each
+// per scattering vertex)
 template <uint32_t FT>
 RT_D float lights_pdf(const DevScene& sc, f3 origin, f3 dir) {
   float sum = 0.0f;
-  for (int i = 0; i < sc.n_lights; ++i) {  // uniform loop: the table entry is a scalar load
-    const F4 e = FT != FT_ALL ? ld_cst((const F4*)sc.lights + __builtin_amdgcn_readfirstlane(i))
-                              : ((const F4*)sc.lights)[i];
+#ifdef RT_LIGHTS_SGPR  // (A/B builds: the light table's fields as the compiler holds them)
+  const int n_lights = sc.n_lights;
+  const DevLight* lights = sc.lights;
+#else
+  const cst_params* kp = kparams();
+  const int n_lights = kp->sc.n_lights;
+  const DevLight* lights = kp->sc.lights;
+#endif
+  for (int i = 0; i < n_lights; ++i) {  // uniform loop: the table entry is a scalar load
+    const F4 e = FT != FT_ALL ? ld_cst((const F4*)lights + __builtin_amdgcn_readfirstlane(i))
+                              : ((const F4*)lights)[i];
     const uint32_t ref = fbits(e.x);
     if (ref == PRIM_NONE) continue;
     sum += e.z * prim_pdf<FT>(sc, ref, i, origin, dir);
@@ -1482,16 +1511,26 @@ RT_D float lights_pdf(const DevScene& sc, f3 origin, f3 dir) {
 template <uint32_t FT>
 RT_D f3 lights_random(const DevScene& sc, f3 origin, const rt_u32x4& r) {
   const float s0 = rt_unit_f(r.v[2]), s1 = rt_unit_f(r.v[3]);
-  int lo = 0, hi = sc.n_lights - 1;
-  if (sc.n_lights <= 0) return mk3(rt_unit_f(r.v[1]), s0, s1);  // vec.Random()
+#ifdef RT_LIGHTS_SGPR
+  const int n_lights = sc.n_lights;
+  const DevLight* lights = sc.lights;
+  const F4* light_recs = sc.light_recs;
+#else
+  const cst_params* kp = kparams();  // (as lights_pdf)
+  const int n_lights = kp->sc.n_lights;
+  const DevLight* lights = kp->sc.lights;
+  const F4* light_recs = kp->sc.light_recs;
+#endif
+  int lo = 0, hi = n_lights - 1;
+  if (n_lights <= 0) return mk3(rt_unit_f(r.v[1]), s0, s1);  // vec.Random()
   const uint32_t u24 = rt_u24(r.v[1]);
   while (lo < hi) {  // last entry with lo24 <= u24
     int mid = (lo + hi + 1) >> 1;
-    if (sc.lights[mid].lo24 <= u24) lo = mid;
+    if (lights[mid].lo24 <= u24) lo = mid;
     else hi = mid - 1;
   }
   const uint32_t ref =
-      FT != FT_ALL && sc.n_lights == 1 ? fbits(ld_cst((const F4*)sc.lights).x) : sc.lights[lo].ref;
+      FT != FT_ALL && n_lights == 1 ? fbits(ld_cst((const F4*)lights).x) : lights[lo].ref;
   if (ref == PRIM_NONE) return mk3(rt_unit_f(r.v[1]), s0, s1);
   uint32_t type = ref >> 30, idx = ref & 0x3FFFFFFFu;
   if (HAS(FT_SPHERE) && type == PRIM_SPHERE) {  // sphere.Random + randomToSphere objects.go:63-80
@@ -1506,11 +1545,11 @@ RT_D f3 lights_random(const DevScene& sc, f3 origin, const rt_u32x4& r) {
   if (!HAS(FT_TRI) || type == PRIM_QUAD) {  // quad.Random objects.go:161-165
     // the light record's Q, u, v; one light: a uniform index, so scalar loads
     F4 Q, U, V;
-    if (FT != FT_ALL && sc.n_lights == 1) {
-      const F4* lr = sc.light_recs + 4;
+    if (FT != FT_ALL && n_lights == 1) {
+      const F4* lr = light_recs + 4;
       Q = ld_cst(lr), U = ld_cst(lr + 1), V = ld_cst(lr + 2);
     } else {
-      const F4* lr = sc.light_recs + 8 * (size_t)lo + 4;
+      const F4* lr = light_recs + 8 * (size_t)lo + 4;
       Q = lr[0], U = lr[1], V = lr[2];
     }
     return (xyz(Q) + xyz(U) * s0 + xyz(V) * s1) - origin;
@@ -1682,7 +1721,7 @@ struct WStack {
       q[nlds * 256] = v.y;
       q[2 * nlds * 256] = v.z;
     } else {
-      st_glb(P.stack + hbm_index(P, slot, k), v);
+      st_glb(hbm_entry(P, slot, k), v);
     }
   }
   // entry k (the top) *= w: a dominated clamp vertex merged into it (shade_core);
@@ -1696,7 +1735,7 @@ struct WStack {
       q[nlds * 256] = r.y;
       q[2 * nlds * 256] = r.z;
     } else {
-      F4* e = P.stack + hbm_index(P, slot, k);
+      F4* e = hbm_entry(P, slot, k);
       const F4 v = ld_glb(e);
       r = mk3(v.x * w.x, v.y * w.y, v.z * w.z);
       st_glb(e, {r.x, r.y, r.z, 0.0f});
@@ -1705,6 +1744,17 @@ struct WStack {
   }
   // HBM entries: [entry][slot] (a wave's lanes at one depth coalesce) or, with
   // WSTACK_SLOT_MAJOR, [slot][entry] (one lane's pushes share cache lines)
+  // the entry's address, with the stack base and column count re-read from the
+  // kernel-argument segment (kparams): these rare HBM branches otherwise kept a 64-bit base
+  // live across the fused loop (2 spilled VGPRs in the record-loop kernel)
+  RT_D F4* hbm_entry(const Params& P, uint32_t slot, uint32_t k) const {
+    const cst_params* kp = kparams();
+#ifdef WSTACK_SLOT_MAJOR
+    return kp->stack + ((size_t)slot * (kp->max_depth + 1) + (k - nlds));
+#else
+    return kp->stack + ((size_t)(k - nlds) * kp->P + slot);
+#endif
+  }
   RT_D size_t hbm_index(const Params& P, uint32_t slot, uint32_t k) const {
 #ifdef WSTACK_SLOT_MAJOR
     return (size_t)slot * (P.max_depth + 1) + (k - nlds);
@@ -1727,8 +1777,8 @@ struct WStack {
 #ifndef RT_FOLD_ONE_LOAD
     // HBM entries two at a time: both loads in flight before the products need them
     for (; k - 1 >= nlds; k -= 2) {
-      const F4 a = ld_glb(P.stack + hbm_index(P, slot, (uint32_t)k));
-      const F4 b = ld_glb(P.stack + hbm_index(P, slot, (uint32_t)(k - 1)));
+      const F4 a = ld_glb(hbm_entry(P, slot, (uint32_t)k));
+      const F4 b = ld_glb(hbm_entry(P, slot, (uint32_t)(k - 1)));
       v = xyz(a) * v;
       maxI = fmaxf(maxI, v.x + v.y + v.z);
       v = xyz(b) * v;
@@ -1736,7 +1786,7 @@ struct WStack {
     }
 #endif
     for (; k >= nlds; --k) {
-      v = xyz(ld_glb(P.stack + hbm_index(P, slot, (uint32_t)k))) * v;
+      v = xyz(ld_glb(hbm_entry(P, slot, (uint32_t)k))) * v;
       maxI = fmaxf(maxI, v.x + v.y + v.z);
     }
     if (nlds > 0 && nst > 0) {
@@ -1757,7 +1807,7 @@ struct WStack {
   // the step-by-step fold (A/B builds: -DRT_FOLD_STEPWISE)
   RT_D f3 fold(const Params& P, uint32_t slot, uint32_t nst, f3 L) const {
     for (int k = (int)nst - 1; k >= nlds; --k)
-      L = clamp_contribution(xyz(ld_glb(P.stack + hbm_index(P, slot, (uint32_t)k))) * L, P.maxc);
+      L = clamp_contribution(xyz(ld_glb(hbm_entry(P, slot, (uint32_t)k))) * L, P.maxc);
     if (nlds > 0 && nst > 0) {
       const lds_f32* q = (const lds_f32*)lds;
       f3 e[kLdsWMax];

@@ -1,5 +1,5 @@
 """Quick GPU timing probe: render a config once and print throughput (dev tool).
-usage: gpu_probe.py scene width spp [modes] [aspect]"""
+usage: gpu_probe.py scene width spp [modes] [aspect]   (CHUNK=K: samples per chunk)"""
 import sys, time, json
 sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 import go_raytracer_amd as rt
@@ -21,7 +21,8 @@ with rt.Scene(t, w, l) as sc:
         sc.render(cam, seed=1, mode=mode)  # warm: upload + state buffers
         cam.SamplesPerPixel = spp
         t0 = time.time()
-        img, st = sc.render(cam, seed=1, profile=True, mode=mode)
+        kw = {"chunk": int(__import__("os").environ["CHUNK"])} if __import__("os").environ.get("CHUNK") else {}
+        img, st = sc.render(cam, seed=1, profile=True, mode=mode, **kw)
         dt = time.time() - t0
         print(json.dumps({"scene": scene, "mode": mode, "W": width, "spp": spp, "s": round(dt, 4),
                           "Msamples_s": round(st["samples"] / dt / 1e6, 2),
