@@ -41,6 +41,7 @@ constexpr Knob kKnobs[] = {
     {"RT_BRUTE_AXIS", false},      // 0: no axis-aligned record groups
     {"RT_BRUTE_VERT", false},      // 0: no y-parallel record group
     {"RT_BRUTE_BOX", true},        // 0: boxes as six records instead of one slab test
+    {"RT_BRUTE_MIXED", false},     // 0: two odd axis-aligned records join the general pairs
     {"RT_SHADE_LDS", false},       // 0: no LDS shade table for the lean record loop
     // every render (rt_render.hip render_impl)
     {"RT_TREE", true},             // 2 / 4: force the BVH2 / BVH4 over the record loop

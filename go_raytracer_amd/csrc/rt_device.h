@@ -189,6 +189,9 @@ struct DevScene {
                         // (boxes rotated about y, tested as slabs: rt_path.h brute_box),
                         // then the boxes' face records (not looped over)
   int32_t brute_ng;     // record loop: general pairs (the first ones)
+  int32_t brute_mx;     // record loop: a mixed pair after the axis-aligned ones, two axis-aligned
+                        // records of axes a0 < a1 (rt_path.h brute_mixed): (a0+1) | (a1+1) << 2,
+                        // 0 when there is none
   float pdf_floor;      // 1e-30 when every light entry is a prim, else 0 (rt_path.h shade)
   int32_t n_perlins;    // perlin 0's tables are staged in LDS by the noise kernels
   int32_t merge_ok;     // every weight and radiance is >= 0 (solid colours, metal albedos

@@ -61,6 +61,26 @@ RT_D void finish_hit(const Params& P, const Path& s, Hit& best) {
 #ifndef TRI_WAVES
 #define TRI_WAVES 4
 #endif
+#ifndef TRI_QWAVES
+// the {sphere, triangle, metal} set (C5) on the compressed BVH4 at 5 waves per SIMD (round
+// 5): that kernel needs 113 VGPRs at 4, and 5 waves (96 VGPRs, 6 spilled; 12 LDS stack
+// entries, TRI_QSHORT, so five blocks fit the CU's LDS) measured C5 -3.8 %
+// (profiles/r5_c4_c5_isolation_ab.jsonl); round 2's 5-wave try of the 128-B-node kernel
+// spilled 32 VGPRs in the traversal loop and lost 24 %
+#define TRI_QWAVES 5
+#endif
+#ifndef TRI_QSHORT
+#define TRI_QSHORT 12
+#endif
+#ifndef MESH_QWAVES
+// book1's set (C3) on the compressed BVH4 at 5 waves too (96 VGPRs, 26 spilled, 12 LDS stack
+// entries): C3 -1.2 % (profiles/r5_waves5_ab.jsonl); book2's set at 5 waves lost 3 % (31
+// spilled), it stays at 4
+#define MESH_QWAVES 5
+#endif
+#ifndef MESH_QSHORT
+#define MESH_QSHORT 12
+#endif
 #ifndef FT_TEX_WAVES
 #define FT_TEX_WAVES 4
 #endif
@@ -73,8 +93,8 @@ constexpr int fused_waves(uint32_t ft, int tree = 4) {
   return (tree == 0 && ft == 0u) ? kBruteWaves  // 7 measured within noise of 6, 8 -3 %
          : ft == 0u ? 6
          : ft == FT_MEDIA ? 4
-         : ft == (FT_SPHERE | FT_TRI | FT_METAL) ? TRI_WAVES
-         : ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? MESH_WAVES
+         : ft == (FT_SPHERE | FT_TRI | FT_METAL) ? (tree == 5 ? TRI_QWAVES : TRI_WAVES)
+         : ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? (tree == 5 ? MESH_QWAVES : MESH_WAVES)
          : ft == FT_SET_BOOK2 ? FT_TEX_WAVES
                                                                                   : 3;
 }
@@ -121,8 +141,8 @@ constexpr int fused_wlds(uint32_t ft, int tree = 4) {
 constexpr int fused_short(uint32_t ft, int tree = 4) {
   return tree == 0                                                    ? 0
          : ft == 0u                                                   ? kShortStackMin
-         : ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? MESH_SHORT
-         : ft == (FT_SPHERE | FT_TRI | FT_METAL)                      ? TRI_SHORT
+         : ft == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER) ? (tree == 5 ? MESH_QSHORT : MESH_SHORT)
+         : ft == (FT_SPHERE | FT_TRI | FT_METAL)                      ? (tree == 5 ? TRI_QSHORT : TRI_SHORT)
          : ft == FT_SET_BOOK2 ? TEX_SHORT
                                                                       : kShortStack;
 }

@@ -490,16 +490,10 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
       const bool leaf = (cur & LEAF_BIT) != 0u;
       const F4* it = (const F4*)((const char*)sc.nodes + ((cur & 0x0FFFFFFFu) << 6));
       F4 v[4];
+      // (all four unconditionally: a leaf lane skipping the fourth when the scene has no
+      // quads made hipcc wait for the first loads before the predicated one, C5 +1.9 %)
 #pragma unroll
-      for (int e = 0; e < 3; ++e) v[e] = ld_glb(it + e);
-      // a leaf record's fourth vector is read by quad and box tests only: without quads
-      // in the scene (C5's mesh) a leaf lane fetches 48 B
-#ifdef RT_LEAF64  // (A/B builds: every leaf lane fetches 64 B)
-      v[3] = ld_glb(it + 3);
-#else
-      v[3] = F4{0.0f, 0.0f, 0.0f, 0.0f};
-      if (!leaf || HAS(FT_BOX) || sc.quad != nullptr) v[3] = ld_glb(it + 3);
-#endif
+      for (int e = 0; e < 4; ++e) v[e] = ld_glb(it + e);
       if (!leaf) {
         // t = off * inv + (corner - o) * inv per plane (v_fma_mix_f32 on the fp16 offset).
         // Planes come as (lo 0|1, lo 2|3, hi 0|1, hi 2|3) per axis; the near pair is lo when
@@ -1006,6 +1000,42 @@ RT_D void brute_axis(const DevScene& sc, const F4* lrec, int p0, int p1, const v
     bk = pick_by(k1, bk, m1);
   }
 }
+// A mixed pair: record 2p axis-aligned on A0, record 2p+1 on A1 (A0 < A1; the odd records of
+// two axis groups, host-paired).  Each half runs brute_axis's arithmetic on its own axis --
+// the same operations on the same operands, so the same t, alpha, beta bit for bit -- with the
+// ray's components gathered per half ({o[A0], o[A1]}, ...) and the records' in-plane fields
+// gathered per half by pair selects.
+template <int A0, int A1, bool SMEM>
+RT_D void brute_mixed(const DevScene& sc, const F4* lrec, int p0, int p1, const v2f* O,
+                      const v2f* Dv, float tmin, float& best, uint32_t& bk) {
+  constexpr int B00 = A0 == 0 ? 1 : 0, B10 = A0 == 2 ? 1 : 2;  // in-plane axes of half 0
+  constexpr int B01 = A1 == 0 ? 1 : 0, B11 = A1 == 2 ? 1 : 2;  // ... of half 1
+  const float d0 = Dv[A0].x, d1 = Dv[A1].x;
+  const v2f inv = {fabsf(d0) >= 1e-8f ? rcp(d0) : __builtin_nanf(""),
+                   fabsf(d1) >= 1e-8f ? rcp(d1) : __builtin_nanf("")};
+  const v2f Oa = {O[A0].x, O[A1].x};
+  const v2f Ob0 = {O[B00].x, O[B01].x}, Ob1 = {O[B10].x, O[B11].x};
+  const v2f Db0 = {Dv[B00].x, Dv[B01].x}, Db1 = {Dv[B10].x, Dv[B11].x};
+  for (int p = p0; p < p1; ++p) {
+    v4f r[7];
+    load_pair<SMEM>(sc, lrec, p, r);
+    const uint32_t k0 = __float_as_uint(r[6].z), k1 = __float_as_uint(r[6].w);
+    const v2f t = (r[1].zw - Oa) * inv;
+    const v2f q0 = {pair_q<B00>(r).x, pair_q<B01>(r).y}, q1 = {pair_q<B10>(r).x, pair_q<B11>(r).y};
+    const v2f a0 = {pair_a<B00>(r).x, pair_a<B01>(r).y}, a1 = {pair_a<B10>(r).x, pair_a<B11>(r).y};
+    const v2f b0 = {pair_b<B00>(r).x, pair_b<B01>(r).y}, b1 = {pair_b<B10>(r).x, pair_b<B11>(r).y};
+    const v2f pb = pfma(Db0, t, Ob0) - q0;
+    const v2f pc = pfma(Db1, t, Ob1) - q1;
+    const v2f a = pfma(pc, a1, pb * a0);
+    const v2f b = pfma(pc, b1, pb * b0);
+    const uint32_t m0 = rec_reject_t(t.x, tmin, best, a.x, b.x);
+    best = bitsf(pick_by(fbits(t.x), fbits(best), m0));
+    bk = pick_by(k0, bk, m0);
+    const uint32_t m1 = rec_reject_t(t.y, tmin, best, a.y, b.y);
+    best = bitsf(pick_by(fbits(t.y), fbits(best), m1));
+    bk = pick_by(k1, bk, m1);
+  }
+}
 // Pairs parallel to axis AX (host-grouped): n_AX = 0 and A_AX = 0 exactly and B has only
 // its AX component (NewBox's side faces after RotateY: v is the vertical edge).  Each
 // dropped term of the general test is an exact zero, so den, num, alpha and beta are the
@@ -1175,7 +1205,11 @@ RT_D void trav_brute(const DevScene& sc, const F4* lrec, f3 o, f3 d, float time,
   brute_axis<0, SMEM>(sc, lrec, q, q + nax, O, Dv, tmin, best, bk);
   brute_axis<1, SMEM>(sc, lrec, q + nax, q + nax + nay, O, Dv, tmin, best, bk);
   brute_axis<2, SMEM>(sc, lrec, q + nax + nay, q + nax + nay + naz, O, Dv, tmin, best, bk);
-  const int qb = q + nax + nay + naz;
+  const int qm = q + nax + nay + naz, mx = kp->sc.brute_mx;  // the mixed pair (0 or 1)
+  if (mx == (1 | (2 << 2))) brute_mixed<0, 1, SMEM>(sc, lrec, qm, qm + 1, O, Dv, tmin, best, bk);
+  else if (mx == (1 | (3 << 2))) brute_mixed<0, 2, SMEM>(sc, lrec, qm, qm + 1, O, Dv, tmin, best, bk);
+  else if (mx == (2 | (3 << 2))) brute_mixed<1, 2, SMEM>(sc, lrec, qm, qm + 1, O, Dv, tmin, best, bk);
+  const int qb = qm + (mx != 0 ? 1 : 0);
   const float iy = rcp(d.y);
   brute_box<SMEM>(sc, lrec, qb, qb + kp->sc.brute_box, O, Dv, iy, tmin, best, bk);
   if (bk != 0xFFFFFFFFu) {
@@ -1589,19 +1623,22 @@ RT_D unsigned long long to_fixed(float v) {
 // a sample with a channel outside the fixed-point range or non-finite (rare): every
 // channel goes straight to the pixel (fixed-point channels included: the integer sum
 // does not care where it is added)
+// (the buffers' addresses re-read from the kernel-argument segment: held across the fused
+// loop for these rare branches they cost the record-loop kernel spilled VGPRs)
 RT_D void add_sample_rare(const Params& P, uint32_t lp, float x, float y, float z) {
+  const cst_params* kp = kparams();
   const float c[3] = {x, y, z};
   for (int ch = 0; ch < 3; ++ch) {
     const float v = c[ch];
-    if (fabsf(v) < P.vlim) {
-      atomicAdd(&P.accum[(size_t)ch * P.npix + lp], to_fixed(v));
+    if (fabsf(v) < kp->vlim) {
+      atomicAdd(&kp->accum[(size_t)ch * kp->npix + lp], to_fixed(v));
     } else if (isnan(v)) {
-      atomicOr(&P.pflags[lp], 1u << ch);
+      atomicOr(&kp->pflags[lp], 1u << ch);
     } else if (isinf(v)) {
-      atomicOr(&P.pflags[lp], (v > 0.0f ? 8u : 64u) << ch);
+      atomicOr(&kp->pflags[lp], (v > 0.0f ? 8u : 64u) << ch);
     } else {
-      atomicAdd(&P.side[(size_t)ch * P.npix + lp], (double)v);
-      atomicAdd(&P.ctr->overflow, 1ull);
+      atomicAdd(&kp->side[(size_t)ch * kp->npix + lp], (double)v);
+      atomicAdd(&kp->ctr->overflow, 1ull);
     }
   }
 }
@@ -1654,6 +1691,7 @@ struct SampleAcc {
       return;
     }
     const uint32_t lp = local_pixel(P, chunk);
+    const cst_params* kp = kparams();  // (as add_sample_rare: a rare branch)
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
       lds_u64* q = (lds_u64*)lds + ch * 256;
@@ -1665,9 +1703,9 @@ struct SampleAcc {
       if (s)
 #endif
 #ifdef RT_ABLATE_STFLUSH  // timing ablation only (wrong images): plain stores, not atomics
-        P.accum[(size_t)ch * P.npix + lp] = s;
+        kp->accum[(size_t)ch * kp->npix + lp] = s;
 #else
-        atomicAdd(&P.accum[(size_t)ch * P.npix + lp], s);
+        atomicAdd(&kp->accum[(size_t)ch * kp->npix + lp], s);
 #endif
     }
   }

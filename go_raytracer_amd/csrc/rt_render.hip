@@ -642,14 +642,26 @@ static int upload_scene(const Scene* s, DeviceScene* ds) {
       const int v = a < 0 ? vert_of(i) : -1;
       grp[a >= 0 ? a : v >= 0 ? 4 + v : 3].push_back(i);
     }
-    // (Padding an odd axis group with a never-hit record instead, so Cornell's light and back
-    // wall each get an axis pair rather than sharing one general pair, measured 2.5 % slower
-    // on C2 in round 5: one more loop and its per-axis setup cost more than the cheaper test.)
+    // The odd records of two axis-aligned groups of different axes form one mixed pair, each
+    // half tested on its own axis (rt_path.h brute_mixed: the axis test, bit for bit, ~35 VALU
+    // where the general pair was ~85; Cornell's light and back wall).  Any other odd record
+    // joins the general list.  (Padding each odd group with a never-hit record instead measured
+    // 2.5 % slower on C2: one more loop and its per-axis setup.)  RT_BRUTE_MIXED=0: no mixed pair.
+    std::vector<std::pair<int, size_t>> odd_ax;  // (axis, record)
     for (int a : {0, 1, 2, 4, 5, 6})
       if (grp[a].size() & 1) {
-        grp[3].push_back(grp[a].back());  // the group's smallest record
+        if (a < 3 && env_int("RT_BRUTE_MIXED", 1) != 0) odd_ax.push_back({a, grp[a].back()});
+        else grp[3].push_back(grp[a].back());  // the group's smallest record
         grp[a].pop_back();
       }
+    if (odd_ax.size() == 3) {  // the third joins the general list
+      grp[3].push_back(odd_ax.back().second);
+      odd_ax.pop_back();
+    }
+    if (odd_ax.size() == 1) {
+      grp[3].push_back(odd_ax.back().second);
+      odd_ax.clear();
+    }
     std::stable_sort(grp[3].begin(), grp[3].end(),
                      [&](size_t a, size_t b) { return area(h.refs[a]) > area(h.refs[b]); });
     std::vector<long> slots;  // record per slot in loop order, -1 = pad
@@ -664,6 +676,12 @@ static int upload_scene(const Scene* s, DeviceScene* ds) {
     for (int a = 0; a < 3; ++a) {
       for (size_t i : grp[a]) slots.push_back((long)i);
       d.brute_ax[a] = (int32_t)(grp[a].size() / 2);
+    }
+    d.brute_mx = 0;  // the mixed pair (axes a0 < a1): (a0 + 1) | (a1 + 1) << 2
+    if (odd_ax.size() == 2) {
+      slots.push_back((long)odd_ax[0].second);  // odd_ax is in axis order (0, 1, 2 above)
+      slots.push_back((long)odd_ax[1].second);
+      d.brute_mx = (odd_ax[0].first + 1) | ((odd_ax[1].first + 1) << 2);
     }
     const size_t n_loop = slots.size();  // records the loop tests one by one
     // box descriptors, two per pair slot (an odd box count repeats the last box: the
