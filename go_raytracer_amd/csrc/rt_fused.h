@@ -114,12 +114,14 @@ constexpr int fused_waves(uint32_t ft, int tree = 4) {
 #define TRI_WLDS MESH_WLDS
 #endif
 #ifndef TEX_SHORT
-// book2's set: 13 entries fill its 4-wave LDS budget (C4 -1.0 % against 12 at full size;
-// 16 x 3 / 18 x 2 / 21 x 1 stack x weight entries: +0.6 to +1.7 %, r3_tex_stack_ab.jsonl)
-#define TEX_SHORT 13
+// book2's set: 10 traversal-stack and 5 weight entries fill its 4-wave LDS budget with the
+// staged perlin tables (C4 -0.8 % against 13 x 4, +2 % at 7 x 6 on the compressed BVH4,
+// profiles/r5_c4_stack_split_ab.jsonl; round 3 on the 128-B nodes: 16 x 3 / 18 x 2 / 21 x 1
+// +0.6 to +1.7 % against 13 x 4, r3_tex_stack_ab.jsonl)
+#define TEX_SHORT 10
 #endif
 #ifndef TEX_WLDS
-#define TEX_WLDS 4  // book2's set: room for the staged perlin tables at 4 waves/SIMD
+#define TEX_WLDS 5
 #endif
 #ifndef ALL_WLDS
 #define ALL_WLDS 4  // 6 pushed the C3-size trees out of the 3-wave LDS budget
@@ -152,6 +154,9 @@ constexpr unsigned fused_static_lds(uint32_t ft, int tree = 4) {
          ((ft & FT_NOISE) ? 256u * 16u + 768u : 0u);
 }
 __shared__ unsigned long long g_tstart[4];  // per wave: k_fused's start time (RT_WAVE_TIMES)
+#ifdef RT_DRAIN_TIMES
+__shared__ unsigned long long g_tdrain[4];  // debug builds: when the wave's grab came back empty
+#endif
 // TREE: 4 = BVH4, 5 = compressed BVH4 (64-B nodes, global only), 2 = BVH2, 0 = no tree
 // (every record tested, tiny scenes)
 template <bool LDS, uint32_t FT, int TREE>
@@ -190,7 +195,12 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
   WaveBatch b = batch_init(P);
   // debug (RT_WAVE_TIMES): the wave's start time parks in LDS (a register held across the
   // loop for this was the record-loop kernel's one spilled VGPR)
-  if (P.wave_times && lane_id() == 0u) g_tstart[threadIdx.x >> 6] = wall_clock64();
+  // (the wave's index in an SGPR: threadIdx.x >> 6 kept to the end took a spilled VGPR)
+  const uint32_t wave_in_group = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (P.wave_times && lane_id() == 0u) g_tstart[wave_in_group] = wall_clock64();
+#ifdef RT_DRAIN_TIMES
+  if (lane_id() == 0u) g_tdrain[wave_in_group] = 0ull;
+#endif
   // Scheduling round: lanes without work take a chunk; traversing lanes run up
   // to step_budget traversal steps; lanes whose traversal is done are shaded
   // together once at least shade_min of them wait (or nothing else traverses),
@@ -216,6 +226,10 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
       has = true;
     }
     PH_ADD(PH_GRAB, t_grab);
+#ifdef RT_DRAIN_TIMES
+    if (b.part >= (uint32_t)kMaxParts && lane_id() == 0u && g_tdrain[wave_in_group] == 0ull)
+      g_tdrain[wave_in_group] = wall_clock64();
+#endif
     if (!__any(has)) break;
     PH_T(t_trav);
     if (has && tr.cur != TRAV_DONE)
@@ -282,14 +296,18 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
     atomicAdd(&P.ctr->segments, (unsigned long long)segs);
     atomicAdd(&P.ctr->pushes, (unsigned long long)pushes);
     if (P.wave_times) {
-      const size_t w = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+      const size_t w = (size_t)blockIdx.x * 4 + wave_in_group;
       unsigned long long* rec = P.wave_times + kWaveRec * w;
-      rec[0] = g_tstart[threadIdx.x >> 6];
+      rec[0] = g_tstart[wave_in_group];
       rec[1] = wall_clock64();
       rec[2] = segs;
+#ifdef RT_DRAIN_TIMES
+      rec[3] = g_tdrain[wave_in_group];
+#else
       rec[3] = 0ull;
+#endif
 #ifdef RT_PHASES
-      for (int i = 0; i < PH_N; ++i) rec[4 + i] = g_ph[threadIdx.x >> 6][i];
+      for (int i = 0; i < PH_N; ++i) rec[4 + i] = g_ph[wave_in_group][i];
 #else
       for (int i = 0; i < PH_N; ++i) rec[4 + i] = 0ull;
 #endif

@@ -1001,40 +1001,33 @@ RT_D void brute_axis(const DevScene& sc, const F4* lrec, int p0, int p1, const v
   }
 }
 // A mixed pair: record 2p axis-aligned on A0, record 2p+1 on A1 (A0 < A1; the odd records of
-// two axis groups, host-paired).  Each half runs brute_axis's arithmetic on its own axis --
-// the same operations on the same operands, so the same t, alpha, beta bit for bit -- with the
-// ray's components gathered per half ({o[A0], o[A1]}, ...) and the records' in-plane fields
-// gathered per half by pair selects.
+// two axis groups, host-paired; one pair per scene at most).  Each half runs brute_axis's
+// arithmetic on its own axis in scalar form -- the same operations on the same operands
+// (a packed op is two IEEE fp32 ops), so the same t, alpha, beta bit for bit -- reading the
+// ray's components from o and d directly: a packed form gathered {o[A0], o[A1]}, ... into
+// ten new registers, which spilled three VGPRs of the record-loop kernel.
+template <int I> RT_D float comp(f3 v) { return I == 0 ? v.x : I == 1 ? v.y : v.z; }
+template <int A, int H>
+RT_D void brute_half(const v4f* r, f3 o, f3 d, float tmin, float& best, uint32_t& bk) {
+  constexpr int B0 = A == 0 ? 1 : 0, B1 = A == 2 ? 1 : 2;  // in-plane axes, ascending
+  const float da = comp<A>(d);
+  const float ia = fabsf(da) >= 1e-8f ? rcp(da) : __builtin_nanf("");  // |n.d| < 1e-8: no hit
+  const float t = ((H ? r[1].w : r[1].z) - comp<A>(o)) * ia;
+  const float pb = fmaf(comp<B0>(d), t, comp<B0>(o)) - (H ? pair_q<B0>(r).y : pair_q<B0>(r).x);
+  const float pc = fmaf(comp<B1>(d), t, comp<B1>(o)) - (H ? pair_q<B1>(r).y : pair_q<B1>(r).x);
+  const float a = fmaf(pc, H ? pair_a<B1>(r).y : pair_a<B1>(r).x, pb * (H ? pair_a<B0>(r).y : pair_a<B0>(r).x));
+  const float b = fmaf(pc, H ? pair_b<B1>(r).y : pair_b<B1>(r).x, pb * (H ? pair_b<B0>(r).y : pair_b<B0>(r).x));
+  const uint32_t m = rec_reject_t(t, tmin, best, a, b);
+  best = bitsf(pick_by(fbits(t), fbits(best), m));
+  bk = pick_by(__float_as_uint(H ? r[6].w : r[6].z), bk, m);
+}
 template <int A0, int A1, bool SMEM>
-RT_D void brute_mixed(const DevScene& sc, const F4* lrec, int p0, int p1, const v2f* O,
-                      const v2f* Dv, float tmin, float& best, uint32_t& bk) {
-  constexpr int B00 = A0 == 0 ? 1 : 0, B10 = A0 == 2 ? 1 : 2;  // in-plane axes of half 0
-  constexpr int B01 = A1 == 0 ? 1 : 0, B11 = A1 == 2 ? 1 : 2;  // ... of half 1
-  const float d0 = Dv[A0].x, d1 = Dv[A1].x;
-  const v2f inv = {fabsf(d0) >= 1e-8f ? rcp(d0) : __builtin_nanf(""),
-                   fabsf(d1) >= 1e-8f ? rcp(d1) : __builtin_nanf("")};
-  const v2f Oa = {O[A0].x, O[A1].x};
-  const v2f Ob0 = {O[B00].x, O[B01].x}, Ob1 = {O[B10].x, O[B11].x};
-  const v2f Db0 = {Dv[B00].x, Dv[B01].x}, Db1 = {Dv[B10].x, Dv[B11].x};
-  for (int p = p0; p < p1; ++p) {
-    v4f r[7];
-    load_pair<SMEM>(sc, lrec, p, r);
-    const uint32_t k0 = __float_as_uint(r[6].z), k1 = __float_as_uint(r[6].w);
-    const v2f t = (r[1].zw - Oa) * inv;
-    const v2f q0 = {pair_q<B00>(r).x, pair_q<B01>(r).y}, q1 = {pair_q<B10>(r).x, pair_q<B11>(r).y};
-    const v2f a0 = {pair_a<B00>(r).x, pair_a<B01>(r).y}, a1 = {pair_a<B10>(r).x, pair_a<B11>(r).y};
-    const v2f b0 = {pair_b<B00>(r).x, pair_b<B01>(r).y}, b1 = {pair_b<B10>(r).x, pair_b<B11>(r).y};
-    const v2f pb = pfma(Db0, t, Ob0) - q0;
-    const v2f pc = pfma(Db1, t, Ob1) - q1;
-    const v2f a = pfma(pc, a1, pb * a0);
-    const v2f b = pfma(pc, b1, pb * b0);
-    const uint32_t m0 = rec_reject_t(t.x, tmin, best, a.x, b.x);
-    best = bitsf(pick_by(fbits(t.x), fbits(best), m0));
-    bk = pick_by(k0, bk, m0);
-    const uint32_t m1 = rec_reject_t(t.y, tmin, best, a.y, b.y);
-    best = bitsf(pick_by(fbits(t.y), fbits(best), m1));
-    bk = pick_by(k1, bk, m1);
-  }
+RT_D void brute_mixed(const DevScene& sc, const F4* lrec, int p, f3 o, f3 d, float tmin,
+                      float& best, uint32_t& bk) {
+  v4f r[7];
+  load_pair<SMEM>(sc, lrec, p, r);
+  brute_half<A0, 0>(r, o, d, tmin, best, bk);
+  brute_half<A1, 1>(r, o, d, tmin, best, bk);
 }
 // Pairs parallel to axis AX (host-grouped): n_AX = 0 and A_AX = 0 exactly and B has only
 // its AX component (NewBox's side faces after RotateY: v is the vertical edge).  Each
@@ -1206,9 +1199,9 @@ RT_D void trav_brute(const DevScene& sc, const F4* lrec, f3 o, f3 d, float time,
   brute_axis<1, SMEM>(sc, lrec, q + nax, q + nax + nay, O, Dv, tmin, best, bk);
   brute_axis<2, SMEM>(sc, lrec, q + nax + nay, q + nax + nay + naz, O, Dv, tmin, best, bk);
   const int qm = q + nax + nay + naz, mx = kp->sc.brute_mx;  // the mixed pair (0 or 1)
-  if (mx == (1 | (2 << 2))) brute_mixed<0, 1, SMEM>(sc, lrec, qm, qm + 1, O, Dv, tmin, best, bk);
-  else if (mx == (1 | (3 << 2))) brute_mixed<0, 2, SMEM>(sc, lrec, qm, qm + 1, O, Dv, tmin, best, bk);
-  else if (mx == (2 | (3 << 2))) brute_mixed<1, 2, SMEM>(sc, lrec, qm, qm + 1, O, Dv, tmin, best, bk);
+  if (mx == (1 | (2 << 2))) brute_mixed<0, 1, SMEM>(sc, lrec, qm, o, d, tmin, best, bk);
+  else if (mx == (1 | (3 << 2))) brute_mixed<0, 2, SMEM>(sc, lrec, qm, o, d, tmin, best, bk);
+  else if (mx == (2 | (3 << 2))) brute_mixed<1, 2, SMEM>(sc, lrec, qm, o, d, tmin, best, bk);
   const int qb = qm + (mx != 0 ? 1 : 0);
   const float iy = rcp(d.y);
   brute_box<SMEM>(sc, lrec, qb, qb + kp->sc.brute_box, O, Dv, iy, tmin, best, bk);
@@ -1780,6 +1773,26 @@ struct WStack {
     }
     return r;
   }
+  RT_D f3 get(const Params& P, uint32_t slot, uint32_t k) const {
+    if ((int)k < nlds) {
+      const lds_f32* q = (const lds_f32*)lds + k * 256;
+      return mk3(q[0], q[nlds * 256], q[2 * nlds * 256]);
+    }
+    return xyz(ld_glb(hbm_entry(P, slot, k)));
+  }
+  // entry k (the top, whose value t the caller read with get) = t (.) w
+  RT_D f3 mul_known(const Params& P, uint32_t slot, uint32_t k, f3 t, f3 w) const {
+    const f3 r = mk3(t.x * w.x, t.y * w.y, t.z * w.z);
+    if ((int)k < nlds) {
+      lds_f32* q = (lds_f32*)lds + k * 256;
+      q[0] = r.x;
+      q[nlds * 256] = r.y;
+      q[2 * nlds * 256] = r.z;
+    } else {
+      st_glb(hbm_entry(P, slot, k), {r.x, r.y, r.z, 0.0f});
+    }
+    return r;
+  }
   // HBM entries: [entry][slot] (a wave's lanes at one depth coalesce) or, with
   // WSTACK_SLOT_MAJOR, [slot][entry] (one lane's pushes share cache lines)
   // the entry's address, with the stack base and column count re-read from the
@@ -2155,13 +2168,29 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
           // for any sign.
           // (the flag is re-read from the kernel-argument segment here, kparams(): held in
           // an SGPR across the loop it added SGPR spills)
+#ifdef RT_MERGE_GE1
+          bool merge = false;
+          f3 top;
+          if (kparams()->sc.merge_ok && s.nst > 0 && pv.x >= 0.0f && pv.y >= 0.0f && pv.z >= 0.0f) {
+            const bool le1 = pv.x <= 1.0f && pv.y <= 1.0f && pv.z <= 1.0f;
+            if (le1 || (HAS(FT_MEDIA) && pv.x < INFINITY && pv.y < INFINITY && pv.z < INFINITY)) {
+              const f3 t = ws.get(P, slot, s.nst - 1);
+              merge = le1 || (t.x >= 1.0f && t.y >= 1.0f && t.z >= 1.0f && t.x < INFINITY &&
+                              t.y < INFINITY && t.z < INFINITY);
+              if (merge) top = ws.mul_known(P, slot, s.nst - 1, t, pv);
+            }
+          }
+#else
           const bool merge = kparams()->sc.merge_ok && s.nst > 0 && pv.x >= 0.0f && pv.y >= 0.0f &&
                              pv.z >= 0.0f && pv.x <= 1.0f && pv.y <= 1.0f && pv.z <= 1.0f;
+#endif
 #else
           const bool merge = false;
 #endif
           if (merge) {
+#ifndef RT_MERGE_GE1
             f3 top = ws.mul(P, slot, s.nst - 1, pv);
+#endif
             // Kernels with media also cascade: the merged top may itself now be
             // dominated by the new clamp vertex (0 <= top <= 1), so it folds into the
             // entry below, and so on.  Book2's HBM pushes: 309 M -> 126 M (merge) ->
@@ -2313,6 +2342,9 @@ struct WaveBatch {
   uint32_t next, end;   // wave-uniform: positions [next, end) of partition `part`
   uint32_t part;        // the wave's partition; kMaxParts once every partition is used up
   unsigned long long dead;  // partitions known exhausted
+#ifdef RT_GSS
+  uint32_t seen;        // the last position of `part` this wave saw (a lower bound of its counter)
+#endif
 };
 RT_D uint32_t part_end(const Params& P, uint32_t p) {
   const uint32_t gl = P.gran_log2, lg = P.parts_log2;
@@ -2326,7 +2358,11 @@ RT_D uint32_t part_chunk(const Params& P, uint32_t p, uint32_t pos) {
 RT_D WaveBatch batch_init(const Params& P) {
   // wave-uniform (readfirstlane): the batch lives in SGPRs, not in VGPRs of every lane
   const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+#ifdef RT_GSS
+  return {0u, 0u, wave & ((1u << P.parts_log2) - 1u), 0ull, 0u};
+#else
   return {0u, 0u, wave & ((1u << P.parts_log2) - 1u), 0ull};
+#endif
 }
 RT_D uint32_t grab_chunk(const Params& P, WaveBatch& b, bool need) {
   const unsigned long long m = __ballot(need);
@@ -2348,21 +2384,40 @@ RT_D uint32_t grab_chunk(const Params& P, WaveBatch& b, bool need) {
     // up, or marks one more partition dead (at most NP + 1 passes)
     while (b.part < (uint32_t)kMaxParts) {
       const uint32_t endp = part_end(P, b.part);
+#ifdef RT_GSS
+      // guided: near the partition's end the batch shrinks with what is left (at most
+      // endp - seen), so waves do not end the render on positions batched by another wave
+      const uint32_t left_est = endp > b.seen ? endp - b.seen : 0u;
+      const uint32_t want = max(n - avail, min(P.grab_min, max(left_est >> RT_GSS, 1u)));
+#else
       const uint32_t want = max(P.grab_min, n - avail);
+#endif
       uint32_t v = 0u;
       if (lane_id() == leader) v = atomicAdd(&P.ctr->part[b.part * kPartStride], want);
       g = __builtin_amdgcn_readlane(v, leader);
       if (g < endp) {
         gend = min(g + want, endp);
+#ifdef RT_GSS
+        b.seen = gend;
+#endif
         break;
       }
       b.dead |= 1ull << b.part;
       // probe: lane i reads partition i's counter (stale values only read low)
       const uint32_t li = lane_id();
       bool left = false;
+#ifdef RT_GSS
+      uint32_t pos = 0u;
+      if (li < np) {
+        pos = __hip_atomic_load(&P.ctr->part[li * kPartStride], __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+        left = pos < part_end(P, li);
+      }
+#else
       if (li < np)
         left = __hip_atomic_load(&P.ctr->part[li * kPartStride], __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT) < part_end(P, li);
+#endif
       const unsigned long long live = __ballot(left) & ~b.dead;
       if (!live) {
         b.part = (uint32_t)kMaxParts;
@@ -2372,6 +2427,9 @@ RT_D uint32_t grab_chunk(const Params& P, WaveBatch& b, bool need) {
       const uint32_t sh = b.part + 1u;
       const unsigned long long rot = sh >= 64u ? live : ((live >> sh) | (live << (64u - sh)));
       b.part = __builtin_amdgcn_readfirstlane((sh + (uint32_t)(__ffsll((long long)rot) - 1)) & 63u);
+#ifdef RT_GSS
+      b.seen = __builtin_amdgcn_readlane(pos, b.part);
+#endif
     }
     const uint32_t take = r - avail;  // this lane's offset in the new batch (r >= avail)
     if (r >= avail)

@@ -45,15 +45,17 @@ P1_BAR = 0.995
 
 # >= 99.5 % of linear-RGB channels within 2^-10 * max(1, |ref|)
 # ("frac_close") and of 8-bit outputs equal ("q_equal").  Every scene is held to it
-# except the two named here, each with its measured GPU result (profiles/r3_parity_final.jsonl):
+# except the two named here, each with its measured GPU result (round 5,
+# profiles/r5_parity_final.jsonl):
 # on these the paths are chaotic and fp32 and fp64 paths fork after a few bounces
 # whatever the implementation (tools/fork_probe.py).
 P1_EXCEPTIONS = {
-    # the 200-small-spheres feature scene: q_equal fused 0.9941, wavefront 0.9922
+    # the 200-small-spheres feature scene: q_equal fused 0.9941, wavefront 0.9912
     # (frac_close 0.9990 meets P1)
     "cluster": {"q_equal": 0.990},
     # C5, the 1M-triangle metal knot at 1920x1080x1024 (row subsample):
-    # frac_close 0.9946, q_equal 0.9927
+    # frac_close 0.9933 / 0.9931, q_equal 0.9914 / 0.9916 on the two row sets (compressed
+    # BVH4, surface projection; round 4: 0.9946 / 0.9927)
     "model": {"frac_close": 0.993, "q_equal": 0.990},
 }
 

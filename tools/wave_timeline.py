@@ -36,6 +36,17 @@ with rt.Scene(t, w, l) as sc:
             "idle_frac": round(float(np.sum(span - end) / (span * len(a))), 4),
             "segments_p50": q(a[:, 2], 50), "segments_min": int(a[:, 2].min()),
             "segments_max": int(a[:, 2].max())}), flush=True)
+        if a[:, 3].any():  # -DRT_DRAIN_TIMES builds: when each wave's grab came back empty
+            dr = (a[:, 3] - t0) / 100.0
+            left = end - dr
+            print(json.dumps({
+                "nranks": n, "drain_p1_us": round(q(dr, 1), 1), "drain_p50_us": round(q(dr, 50), 1),
+                "drain_p99_us": round(q(dr, 99), 1), "drain_max_us": round(dr.max(), 1),
+                "after_drain_p50_us": round(q(left, 50), 1), "after_drain_p99_us": round(q(left, 99), 1),
+                "after_drain_max_us": round(left.max(), 1),
+                "drain_p50_by_dispatch_round_us": {
+                    int(r): round(float(np.percentile(dr[(np.arange(len(a)) // 4 // 256) % max(len(a) // 4 // 256, 1) == r], 50)), 1)
+                    for r in range(max(len(a) // 4 // 256, 1))}}), flush=True)
         # end times by XCD (workgroups are dispatched round-robin: block % 8) and by the
         # wave's slot in its workgroup (one workgroup per CU slot: its 4 waves, one per SIMD)
         blk = np.arange(len(a)) // 4
