@@ -195,8 +195,10 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
   WaveBatch b = batch_init(P);
   // debug (RT_WAVE_TIMES): the wave's start time parks in LDS (a register held across the
   // loop for this was the record-loop kernel's one spilled VGPR)
-  // (the wave's index in an SGPR: threadIdx.x >> 6 kept to the end took a spilled VGPR)
-  const uint32_t wave_in_group = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // (the record-loop kernel keeps the wave's index in an SGPR: threadIdx.x >> 6 kept to the
+  // end took its one spilled VGPR; the compressed-BVH kernels spill two more VGPRs that way)
+  const uint32_t wave_in_group = (FT == 0u && TREE == 0) ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)
+                                                         : threadIdx.x >> 6;
   if (P.wave_times && lane_id() == 0u) g_tstart[wave_in_group] = wall_clock64();
 #ifdef RT_DRAIN_TIMES
   if (lane_id() == 0u) g_tdrain[wave_in_group] = 0ull;
@@ -249,8 +251,14 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
       else
       {
         // TREE 5: the compressed BVH4 (64-B items, host_qbvh.cpp), read through L1/L2
+#ifdef RT_QSPEC
+        const int nsteps = TREE == 5 ? trav_steps_qspec<FT>(P.sc, ts, s.o, s.d, s.time, 0.001f, tr, P.step_budget)
+                                     : trav_steps<LDS, FT, TREE == 4, false>(
+                                           P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, tr, P.step_budget);
+#else
         const int nsteps = trav_steps<LDS, FT, TREE == 4 || TREE == 5, TREE == 5>(
             P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, tr, P.step_budget);
+#endif
 #ifdef RT_PHASES
         ph_steps(nsteps);
 #endif

@@ -28,6 +28,7 @@ constexpr uint32_t kCountShift = 8;
 // chunk (k_fused's drain, split_samples); its sums go to the pixel with atomics, not to the
 // chunk's record
 constexpr uint32_t F_SPLIT = 0x80u;
+
 #ifdef RT_NO_SPLIT_TREES
 constexpr bool kSplitTrees = false;  // A/B builds: drain splitting in the record-loop kernel only
 #else
@@ -158,7 +159,7 @@ RT_D uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn
 // shares, not the absolute cycles.
 enum { PH_GRAB, PH_TRAV, PH_MEDIA, PH_SHADE, PH_TEX, PH_LIGHT, PH_TERM, PH_LOOP,
        PH_TRAV_LANES, PH_TRAV_ROUNDS, PH_SHADE_LANES, PH_SHADE_ROUNDS, PH_STEP_LANES,
-       PH_STEP_WAVE, PH_N = 14 };
+       PH_STEP_WAVE, PH_QNODE_LANES, PH_QLEAF_LANES, PH_QMIXED, PH_QITERS, PH_N = 18 };
 constexpr int kWaveRec = 4 + PH_N;  // {start, end, segments, pad, phases...} per wave
 #ifdef RT_PHASES
 __shared__ unsigned long long g_ph[4][PH_N];
@@ -443,7 +444,11 @@ RT_D void trav_init(const DevScene& sc, f3 o, f3 d, float time, Trav& tr) {
   tr.inv = mk3(rcp(d.x), rcp(d.y), rcp(d.z));
   tr.cur = sc.root == PRIM_NONE ? TRAV_DONE : sc.root;
   tr.sp = 0;
+#ifdef RT_QSPEC
+  tr.top = TRAV_DONE;  // no parked leaf (trav_steps_qspec)
+#else
   tr.top = 0;
+#endif
   tr.best = {kInf, 0.0f, 0.0f, PRIM_NONE};
   if (HAS(FT_SPHERE))
     for (int i = 0; i < sc.n_big; ++i) {
@@ -460,6 +465,136 @@ RT_D void trav_init(const DevScene& sc, f3 o, f3 d, float time, Trav& tr) {
 // one fp16 half of a 32-bit word as fp32 (an fma on it compiles to v_fma_mix_f32)
 typedef _Float16 h2v __attribute__((ext_vector_type(2)));
 template <int H> RT_D float half_of(uint32_t w) { return (float)__builtin_bit_cast(h2v, w)[H]; }
+
+// The compressed BVH4 node test (trav_steps QN): the four children's entry distances
+// (inf: missed) and codes, sorted front to back
+RT_D void qnode_children(const F4 v[4], f3 o, f3 inv, float tmin, float tmax, float tn[4],
+                         uint32_t ch[4]) {
+  // t = off * inv + (corner - o) * inv per plane (v_fma_mix_f32 on the fp16 offset).
+  // Planes come as (lo 0|1, lo 2|3, hi 0|1, hi 2|3) per axis; the near pair is lo when
+  // inv >= 0 and hi otherwise (a sign-mask select per word), so no min/max per axis.
+  const float bx = (v[0].x - o.x) * inv.x, by = (v[0].y - o.y) * inv.y,
+              bz = (v[0].z - o.z) * inv.z;
+  const uint32_t info = fbits(v[0].w);
+  const uint32_t base = info & 0x0FFFFFFFu, lmask = info >> 28;
+  const uint32_t mx = neg_mask(inv.x), my = neg_mask(inv.y), mz = neg_mask(inv.z);
+  const uint32_t nx[2] = {pick_by(fbits(v[1].x), fbits(v[1].z), mx), pick_by(fbits(v[1].y), fbits(v[1].w), mx)};
+  const uint32_t fx[2] = {pick_by(fbits(v[1].z), fbits(v[1].x), mx), pick_by(fbits(v[1].w), fbits(v[1].y), mx)};
+  const uint32_t ny[2] = {pick_by(fbits(v[2].x), fbits(v[2].z), my), pick_by(fbits(v[2].y), fbits(v[2].w), my)};
+  const uint32_t fy[2] = {pick_by(fbits(v[2].z), fbits(v[2].x), my), pick_by(fbits(v[2].w), fbits(v[2].y), my)};
+  const uint32_t nz[2] = {pick_by(fbits(v[3].x), fbits(v[3].z), mz), pick_by(fbits(v[3].y), fbits(v[3].w), mz)};
+  const uint32_t fz[2] = {pick_by(fbits(v[3].z), fbits(v[3].x), mz), pick_by(fbits(v[3].w), fbits(v[3].y), mz)};
+  auto child = [&](auto hk, int k) {
+    constexpr int H = decltype(hk)::value;
+    const int w = k >> 1;
+    const float tx0 = fmaf(half_of<H>(nx[w]), inv.x, bx), tx1 = fmaf(half_of<H>(fx[w]), inv.x, bx);
+    const float ty0 = fmaf(half_of<H>(ny[w]), inv.y, by), ty1 = fmaf(half_of<H>(fy[w]), inv.y, by);
+    const float tz0 = fmaf(half_of<H>(nz[w]), inv.z, bz), tz1 = fmaf(half_of<H>(fz[w]), inv.z, bz);
+    const float t0 = fmaxf(fmaxf(tx0, ty0), fmaxf(tz0, tmin));
+    const float t1 = fminf(fminf(tx1, ty1), fminf(tz1, tmax));
+    tn[k] = bitsf(pick_by(fbits(t0), 0x7F800000u, neg_mask(t1 * 1.00000024f - t0)));
+    ch[k] = (base + (uint32_t)k) | (((lmask >> k) & 1u) << 31);
+  };
+  child(std::integral_constant<int, 0>{}, 0);
+  child(std::integral_constant<int, 1>{}, 1);
+  child(std::integral_constant<int, 0>{}, 2);
+  child(std::integral_constant<int, 1>{}, 3);
+  auto cx = [&](int a, int b) {  // as the 128-B path's network
+    const uint32_t m = neg_mask(tn[b] - tn[a]);
+    const uint32_t ta = fbits(tn[a]), tb = fbits(tn[b]);
+    const uint32_t ca = ch[a], cb = ch[b];
+    tn[a] = bitsf(pick_by(ta, tb, m));
+    tn[b] = bitsf(pick_by(tb, ta, m));
+    ch[a] = pick_by(ca, cb, m);
+    ch[b] = pick_by(cb, ca, m);
+  };
+  cx(0, 1);
+  cx(2, 3);
+  cx(0, 2);
+  cx(1, 3);
+  cx(1, 2);
+}
+
+#ifdef RT_QSPEC
+// closest-hit update from a reject mask, ties (equal t) going to the larger prim ref: the
+// result is the minimum of (t, -ref) over the prims tested, whatever their order
+RT_D void take_hit(Trav& tr, uint32_t rej, float t, float u, float v, uint32_t ref) {
+  rej |= (t == tr.best.t && ref <= tr.best.ref) ? ~0u : 0u;
+  tr.best.t = bitsf(pick_by(fbits(t), fbits(tr.best.t), rej));
+  tr.best.u = bitsf(pick_by(fbits(u), fbits(tr.best.u), rej));
+  tr.best.v = bitsf(pick_by(fbits(v), fbits(tr.best.v), rej));
+  tr.best.ref = pick_by(ref, tr.best.ref, rej);
+}
+// The compressed BVH4 with postponed leaves (Aila & Laine's speculative traversal): a lane
+// that reaches a leaf parks it (tr.top, one per lane) and goes on with its next node; the
+// wave runs node steps while any lane is still without a parked leaf, then one leaf step for
+// every lane holding one.  A step is then all nodes or all leaves -- one kind of load and
+// one branch -- instead of both in every step where the wave's lanes differ.  Leaves are
+// tested out of traversal order, so ties go by ref (take_hit).
+template <uint32_t FT>
+RT_D int trav_steps_qspec(const DevScene& sc, const TravStack& stack, f3 o, f3 d, float time,
+                          float tmin, Trav& tr, int budget) {
+  uint32_t cur = tr.cur, pend = tr.top;
+  int sp = tr.sp;
+  const f3 inv = tr.inv;
+  int n = 0;
+  for (; n < budget && (cur != TRAV_DONE || pend != TRAV_DONE); ++n) {
+    if (cur != TRAV_DONE && (cur & LEAF_BIT) && pend == TRAV_DONE) {
+      pend = cur;
+      cur = sp == 0 ? TRAV_DONE : stack.pop(--sp);
+    }
+    const bool searching = pend == TRAV_DONE && cur != TRAV_DONE;
+    if (__any(searching)) {
+      if (cur == TRAV_DONE || (cur & LEAF_BIT)) continue;  // a parked leaf and a leaf next
+      const F4* it = (const F4*)((const char*)sc.nodes + (cur << 6));
+      F4 v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = ld_glb(it + e);
+      float tn[4];
+      uint32_t ch[4];
+      qnode_children(v, o, inv, tmin, tr.best.t, tn, ch);
+      if (tn[0] != kInf) {
+        if (sp + 3 <= stack.nshort) {
+          lds_u32* q = (lds_u32*)stack.lds;
+          q[sp * 256] = ch[3];
+          sp += tn[3] != kInf;
+          q[sp * 256] = ch[2];
+          sp += tn[2] != kInf;
+          q[sp * 256] = ch[1];
+          sp += tn[1] != kInf;
+        } else {
+          if (tn[3] != kInf && sp < kStack) stack.push(sp++, ch[3]);
+          if (tn[2] != kInf && sp < kStack) stack.push(sp++, ch[2]);
+          if (tn[1] != kInf && sp < kStack) stack.push(sp++, ch[1]);
+        }
+        cur = ch[0];
+      } else {
+        cur = sp == 0 ? TRAV_DONE : stack.pop(--sp);
+      }
+    } else if (pend != TRAV_DONE) {
+      const F4* it = (const F4*)((const char*)sc.nodes + ((pend & 0x0FFFFFFFu) << 6));
+      F4 v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = ld_glb(it + e);
+      float t, u, vv;
+      uint32_t ref;
+      const uint32_t rej = hit_record_m<FT>(v, o, d, inv.y, time, tmin, tr.best.t, t, u, vv, ref);
+      take_hit(tr, rej, t, u, vv, ref);
+      pend = TRAV_DONE;
+    }
+  }
+  // a budget cut with only a parked leaf left: hand it back as the current item (the next
+  // call parks it again), so "cur == TRAV_DONE" keeps meaning "traversal finished"
+  if (cur == TRAV_DONE && pend != TRAV_DONE) {
+    cur = pend;
+    pend = TRAV_DONE;
+  }
+  tr.cur = cur;
+  tr.sp = sp;
+  tr.top = pend;
+  return n;
+}
+#endif
 
 // QN: the compressed BVH4 (host_qbvh.cpp, rt_device.h "compressed BVH4 node"), 64-B
 // items read through L1/L2; cur = item index, LEAF_BIT set for a single-prim leaf record
@@ -488,6 +623,15 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
     if constexpr (QN) {
       // One 64-B item per step, node or leaf record alike (4 x 16 B, issued together).
       const bool leaf = (cur & LEAF_BIT) != 0u;
+#ifdef RT_PHASES
+      {  // node / leaf steps of this iteration, and whether both kinds ran in it
+        const unsigned long long ml = __ballot(leaf), mn = __ballot(!leaf);
+        PH_CNT(PH_QLEAF_LANES, __popcll(ml));
+        PH_CNT(PH_QNODE_LANES, __popcll(mn));
+        PH_CNT(PH_QMIXED, (ml && mn) ? 1 : 0);
+        PH_CNT(PH_QITERS, 1);
+      }
+#endif
       const F4* it = (const F4*)((const char*)sc.nodes + ((cur & 0x0FFFFFFFu) << 6));
       F4 v[4];
       // (all four unconditionally: a leaf lane skipping the fourth when the scene has no
@@ -495,52 +639,9 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = ld_glb(it + e);
       if (!leaf) {
-        // t = off * inv + (corner - o) * inv per plane (v_fma_mix_f32 on the fp16 offset).
-        // Planes come as (lo 0|1, lo 2|3, hi 0|1, hi 2|3) per axis; the near pair is lo when
-        // inv >= 0 and hi otherwise (a sign-mask select per word), so no min/max per axis.
-        const float bx = (v[0].x - o.x) * inv.x, by = (v[0].y - o.y) * inv.y,
-                    bz = (v[0].z - o.z) * inv.z;
-        const uint32_t info = fbits(v[0].w);
-        const uint32_t base = info & 0x0FFFFFFFu, lmask = info >> 28;
-        const uint32_t mx = neg_mask(inv.x), my = neg_mask(inv.y), mz = neg_mask(inv.z);
-        const uint32_t nx[2] = {pick_by(fbits(v[1].x), fbits(v[1].z), mx), pick_by(fbits(v[1].y), fbits(v[1].w), mx)};
-        const uint32_t fx[2] = {pick_by(fbits(v[1].z), fbits(v[1].x), mx), pick_by(fbits(v[1].w), fbits(v[1].y), mx)};
-        const uint32_t ny[2] = {pick_by(fbits(v[2].x), fbits(v[2].z), my), pick_by(fbits(v[2].y), fbits(v[2].w), my)};
-        const uint32_t fy[2] = {pick_by(fbits(v[2].z), fbits(v[2].x), my), pick_by(fbits(v[2].w), fbits(v[2].y), my)};
-        const uint32_t nz[2] = {pick_by(fbits(v[3].x), fbits(v[3].z), mz), pick_by(fbits(v[3].y), fbits(v[3].w), mz)};
-        const uint32_t fz[2] = {pick_by(fbits(v[3].z), fbits(v[3].x), mz), pick_by(fbits(v[3].w), fbits(v[3].y), mz)};
-        const float tmax = tr.best.t;
         float tn[4];
         uint32_t ch[4];
-        auto child = [&](auto hk, int k) {
-          constexpr int H = decltype(hk)::value;
-          const int w = k >> 1;
-          const float tx0 = fmaf(half_of<H>(nx[w]), inv.x, bx), tx1 = fmaf(half_of<H>(fx[w]), inv.x, bx);
-          const float ty0 = fmaf(half_of<H>(ny[w]), inv.y, by), ty1 = fmaf(half_of<H>(fy[w]), inv.y, by);
-          const float tz0 = fmaf(half_of<H>(nz[w]), inv.z, bz), tz1 = fmaf(half_of<H>(fz[w]), inv.z, bz);
-          const float t0 = fmaxf(fmaxf(tx0, ty0), fmaxf(tz0, tmin));
-          const float t1 = fminf(fminf(tx1, ty1), fminf(tz1, tmax));
-          tn[k] = bitsf(pick_by(fbits(t0), 0x7F800000u, neg_mask(t1 * 1.00000024f - t0)));
-          ch[k] = (base + (uint32_t)k) | (((lmask >> k) & 1u) << 31);
-        };
-        child(std::integral_constant<int, 0>{}, 0);
-        child(std::integral_constant<int, 1>{}, 1);
-        child(std::integral_constant<int, 0>{}, 2);
-        child(std::integral_constant<int, 1>{}, 3);
-        auto cx = [&](int a, int b) {  // as the 128-B path's network
-          const uint32_t m = neg_mask(tn[b] - tn[a]);
-          const uint32_t ta = fbits(tn[a]), tb = fbits(tn[b]);
-          const uint32_t ca = ch[a], cb = ch[b];
-          tn[a] = bitsf(pick_by(ta, tb, m));
-          tn[b] = bitsf(pick_by(tb, ta, m));
-          ch[a] = pick_by(ca, cb, m);
-          ch[b] = pick_by(cb, ca, m);
-        };
-        cx(0, 1);
-        cx(2, 3);
-        cx(0, 2);
-        cx(1, 3);
-        cx(1, 2);
+        qnode_children(v, o, inv, tmin, tr.best.t, tn, ch);
         if (tn[0] != kInf) {
           if (sp + 3 <= stack.nshort) {
             lds_u32* q = (lds_u32*)stack.lds;
@@ -562,10 +663,14 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
         float t, u, vv;
         uint32_t ref;
         const uint32_t rej = hit_record_m<FT>(v, o, d, inv.y, time, tmin, tr.best.t, t, u, vv, ref);
+#ifdef RT_QSPEC
+        take_hit(tr, rej, t, u, vv, ref);
+#else
         tr.best.t = bitsf(pick_by(fbits(t), fbits(tr.best.t), rej));
         tr.best.u = bitsf(pick_by(fbits(u), fbits(tr.best.u), rej));
         tr.best.v = bitsf(pick_by(fbits(vv), fbits(tr.best.v), rej));
         tr.best.ref = pick_by(ref, tr.best.ref, rej);
+#endif
       }
       if (sp == 0) cur = TRAV_DONE;
       else cur = stack.pop(--sp);
@@ -675,10 +780,14 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
           float t, u, vv;
           uint32_t ref;
           const uint32_t rej = hit_record_m<FT>(rec, o, d, inv.y, time, tmin, tr.best.t, t, u, vv, ref);
+#ifdef RT_QSPEC
+          take_hit(tr, rej, t, u, vv, ref);
+#else
           tr.best.t = bitsf(pick_by(fbits(t), fbits(tr.best.t), rej));
           tr.best.u = bitsf(pick_by(fbits(u), fbits(tr.best.u), rej));
           tr.best.v = bitsf(pick_by(fbits(vv), fbits(tr.best.v), rej));
           tr.best.ref = pick_by(ref, tr.best.ref, rej);
+#endif
           if (++k >= count) break;
           const F4* q = sc.leafprims + 4 * (size_t)(first + k);
           for (int e = 0; e < 4; ++e) rec[e] = ld_glb(q + e);
@@ -1773,26 +1882,6 @@ struct WStack {
     }
     return r;
   }
-  RT_D f3 get(const Params& P, uint32_t slot, uint32_t k) const {
-    if ((int)k < nlds) {
-      const lds_f32* q = (const lds_f32*)lds + k * 256;
-      return mk3(q[0], q[nlds * 256], q[2 * nlds * 256]);
-    }
-    return xyz(ld_glb(hbm_entry(P, slot, k)));
-  }
-  // entry k (the top, whose value t the caller read with get) = t (.) w
-  RT_D f3 mul_known(const Params& P, uint32_t slot, uint32_t k, f3 t, f3 w) const {
-    const f3 r = mk3(t.x * w.x, t.y * w.y, t.z * w.z);
-    if ((int)k < nlds) {
-      lds_f32* q = (lds_f32*)lds + k * 256;
-      q[0] = r.x;
-      q[nlds * 256] = r.y;
-      q[2 * nlds * 256] = r.z;
-    } else {
-      st_glb(hbm_entry(P, slot, k), {r.x, r.y, r.z, 0.0f});
-    }
-    return r;
-  }
   // HBM entries: [entry][slot] (a wave's lanes at one depth coalesce) or, with
   // WSTACK_SLOT_MAJOR, [slot][entry] (one lane's pushes share cache lines)
   // the entry's address, with the stack base and column count re-read from the
@@ -2168,29 +2257,13 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
           // for any sign.
           // (the flag is re-read from the kernel-argument segment here, kparams(): held in
           // an SGPR across the loop it added SGPR spills)
-#ifdef RT_MERGE_GE1
-          bool merge = false;
-          f3 top;
-          if (kparams()->sc.merge_ok && s.nst > 0 && pv.x >= 0.0f && pv.y >= 0.0f && pv.z >= 0.0f) {
-            const bool le1 = pv.x <= 1.0f && pv.y <= 1.0f && pv.z <= 1.0f;
-            if (le1 || (HAS(FT_MEDIA) && pv.x < INFINITY && pv.y < INFINITY && pv.z < INFINITY)) {
-              const f3 t = ws.get(P, slot, s.nst - 1);
-              merge = le1 || (t.x >= 1.0f && t.y >= 1.0f && t.z >= 1.0f && t.x < INFINITY &&
-                              t.y < INFINITY && t.z < INFINITY);
-              if (merge) top = ws.mul_known(P, slot, s.nst - 1, t, pv);
-            }
-          }
-#else
           const bool merge = kparams()->sc.merge_ok && s.nst > 0 && pv.x >= 0.0f && pv.y >= 0.0f &&
                              pv.z >= 0.0f && pv.x <= 1.0f && pv.y <= 1.0f && pv.z <= 1.0f;
-#endif
 #else
           const bool merge = false;
 #endif
           if (merge) {
-#ifndef RT_MERGE_GE1
             f3 top = ws.mul(P, slot, s.nst - 1, pv);
-#endif
             // Kernels with media also cascade: the merged top may itself now be
             // dominated by the new clamp vertex (0 <= top <= 1), so it folds into the
             // entry below, and so on.  Book2's HBM pushes: 309 M -> 126 M (merge) ->
@@ -2342,9 +2415,6 @@ struct WaveBatch {
   uint32_t next, end;   // wave-uniform: positions [next, end) of partition `part`
   uint32_t part;        // the wave's partition; kMaxParts once every partition is used up
   unsigned long long dead;  // partitions known exhausted
-#ifdef RT_GSS
-  uint32_t seen;        // the last position of `part` this wave saw (a lower bound of its counter)
-#endif
 };
 RT_D uint32_t part_end(const Params& P, uint32_t p) {
   const uint32_t gl = P.gran_log2, lg = P.parts_log2;
@@ -2358,11 +2428,7 @@ RT_D uint32_t part_chunk(const Params& P, uint32_t p, uint32_t pos) {
 RT_D WaveBatch batch_init(const Params& P) {
   // wave-uniform (readfirstlane): the batch lives in SGPRs, not in VGPRs of every lane
   const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
-#ifdef RT_GSS
-  return {0u, 0u, wave & ((1u << P.parts_log2) - 1u), 0ull, 0u};
-#else
   return {0u, 0u, wave & ((1u << P.parts_log2) - 1u), 0ull};
-#endif
 }
 RT_D uint32_t grab_chunk(const Params& P, WaveBatch& b, bool need) {
   const unsigned long long m = __ballot(need);
@@ -2384,40 +2450,21 @@ RT_D uint32_t grab_chunk(const Params& P, WaveBatch& b, bool need) {
     // up, or marks one more partition dead (at most NP + 1 passes)
     while (b.part < (uint32_t)kMaxParts) {
       const uint32_t endp = part_end(P, b.part);
-#ifdef RT_GSS
-      // guided: near the partition's end the batch shrinks with what is left (at most
-      // endp - seen), so waves do not end the render on positions batched by another wave
-      const uint32_t left_est = endp > b.seen ? endp - b.seen : 0u;
-      const uint32_t want = max(n - avail, min(P.grab_min, max(left_est >> RT_GSS, 1u)));
-#else
       const uint32_t want = max(P.grab_min, n - avail);
-#endif
       uint32_t v = 0u;
       if (lane_id() == leader) v = atomicAdd(&P.ctr->part[b.part * kPartStride], want);
       g = __builtin_amdgcn_readlane(v, leader);
       if (g < endp) {
         gend = min(g + want, endp);
-#ifdef RT_GSS
-        b.seen = gend;
-#endif
         break;
       }
       b.dead |= 1ull << b.part;
       // probe: lane i reads partition i's counter (stale values only read low)
       const uint32_t li = lane_id();
       bool left = false;
-#ifdef RT_GSS
-      uint32_t pos = 0u;
-      if (li < np) {
-        pos = __hip_atomic_load(&P.ctr->part[li * kPartStride], __ATOMIC_RELAXED,
-                                __HIP_MEMORY_SCOPE_AGENT);
-        left = pos < part_end(P, li);
-      }
-#else
       if (li < np)
         left = __hip_atomic_load(&P.ctr->part[li * kPartStride], __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT) < part_end(P, li);
-#endif
       const unsigned long long live = __ballot(left) & ~b.dead;
       if (!live) {
         b.part = (uint32_t)kMaxParts;
@@ -2427,9 +2474,6 @@ RT_D uint32_t grab_chunk(const Params& P, WaveBatch& b, bool need) {
       const uint32_t sh = b.part + 1u;
       const unsigned long long rot = sh >= 64u ? live : ((live >> sh) | (live << (64u - sh)));
       b.part = __builtin_amdgcn_readfirstlane((sh + (uint32_t)(__ffsll((long long)rot) - 1)) & 63u);
-#ifdef RT_GSS
-      b.seen = __builtin_amdgcn_readlane(pos, b.part);
-#endif
     }
     const uint32_t take = r - avail;  // this lane's offset in the new batch (r >= avail)
     if (r >= avail)

@@ -16,7 +16,8 @@ import go_raytracer_amd as rt  # noqa: E402
 rt.tune_from_env()  # dev tool: RT_* knobs from the environment (rt_tune_set)
 
 NAMES = ["grab", "trav", "media", "shade", "tex", "light", "term", "loop",
-         "trav_lanes", "trav_rounds", "shade_lanes", "shade_rounds", "step_lanes", "step_wave"]
+         "trav_lanes", "trav_rounds", "shade_lanes", "shade_rounds", "step_lanes", "step_wave",
+         "qnode_lanes", "qleaf_lanes", "qmixed", "qiters"]
 scene, width, spp = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
 t, cam, w, l = rt.demo_scene(scene)
 cam.Width = width
@@ -31,7 +32,7 @@ with rt.Scene(t, w, l) as sc:
     kw = {"chunk": int(os.environ["CHUNK"])} if "CHUNK" in os.environ else {}
     img, st = sc.render(cam, profile=True, nranks=int(os.environ.get("NRANKS", "1")), **kw)
     rt.untune("RT_WAVE_TIMES")
-a = np.fromfile(path, dtype=np.uint64).reshape(-1, 18).astype(np.float64)
+a = np.fromfile(path, dtype=np.uint64).reshape(-1, 22).astype(np.float64)
 ph = a[:, 4:].sum(axis=0)
 loop = ph[7]
 out = {"scene": scene, "W": width, "spp": spp, "ms": round(st["ms_fused"], 2),
@@ -46,4 +47,8 @@ out["trav_rounds_per_seg"] = round(ph[9] * 64 / max(st["segments"], 1), 3)
 out["steps_per_seg"] = round(ph[12] / max(st["segments"], 1), 2)
 out["step_simd_eff"] = round(ph[12] / max(ph[13], 1) / 64, 4)
 out["cycles_per_seg_wave"] = round(loop / max(st["segments"], 1), 1)
+if ph[17] > 0:  # compressed-BVH kernels: node / leaf lanes per iteration, mixed iterations
+    out["q_node_lanes_per_iter"] = round(ph[14] / ph[17], 2)
+    out["q_leaf_lanes_per_iter"] = round(ph[15] / ph[17], 2)
+    out["q_mixed_iter_frac"] = round(ph[16] / ph[17], 4)
 print(json.dumps(out), flush=True)
