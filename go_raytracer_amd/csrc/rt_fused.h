@@ -251,14 +251,8 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
       else
       {
         // TREE 5: the compressed BVH4 (64-B items, host_qbvh.cpp), read through L1/L2
-#ifdef RT_QSPEC
-        const int nsteps = TREE == 5 ? trav_steps_qspec<FT>(P.sc, ts, s.o, s.d, s.time, 0.001f, tr, P.step_budget)
-                                     : trav_steps<LDS, FT, TREE == 4, false>(
-                                           P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, tr, P.step_budget);
-#else
         const int nsteps = trav_steps<LDS, FT, TREE == 4 || TREE == 5, TREE == 5>(
             P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, tr, P.step_budget);
-#endif
 #ifdef RT_PHASES
         ph_steps(nsteps);
 #endif

@@ -444,11 +444,7 @@ RT_D void trav_init(const DevScene& sc, f3 o, f3 d, float time, Trav& tr) {
   tr.inv = mk3(rcp(d.x), rcp(d.y), rcp(d.z));
   tr.cur = sc.root == PRIM_NONE ? TRAV_DONE : sc.root;
   tr.sp = 0;
-#ifdef RT_QSPEC
-  tr.top = TRAV_DONE;  // no parked leaf (trav_steps_qspec)
-#else
   tr.top = 0;
-#endif
   tr.best = {kInf, 0.0f, 0.0f, PRIM_NONE};
   if (HAS(FT_SPHERE))
     for (int i = 0; i < sc.n_big; ++i) {
@@ -514,87 +510,6 @@ RT_D void qnode_children(const F4 v[4], f3 o, f3 inv, float tmin, float tmax, fl
   cx(1, 3);
   cx(1, 2);
 }
-
-#ifdef RT_QSPEC
-// closest-hit update from a reject mask, ties (equal t) going to the larger prim ref: the
-// result is the minimum of (t, -ref) over the prims tested, whatever their order
-RT_D void take_hit(Trav& tr, uint32_t rej, float t, float u, float v, uint32_t ref) {
-  rej |= (t == tr.best.t && ref <= tr.best.ref) ? ~0u : 0u;
-  tr.best.t = bitsf(pick_by(fbits(t), fbits(tr.best.t), rej));
-  tr.best.u = bitsf(pick_by(fbits(u), fbits(tr.best.u), rej));
-  tr.best.v = bitsf(pick_by(fbits(v), fbits(tr.best.v), rej));
-  tr.best.ref = pick_by(ref, tr.best.ref, rej);
-}
-// The compressed BVH4 with postponed leaves (Aila & Laine's speculative traversal): a lane
-// that reaches a leaf parks it (tr.top, one per lane) and goes on with its next node; the
-// wave runs node steps while any lane is still without a parked leaf, then one leaf step for
-// every lane holding one.  A step is then all nodes or all leaves -- one kind of load and
-// one branch -- instead of both in every step where the wave's lanes differ.  Leaves are
-// tested out of traversal order, so ties go by ref (take_hit).
-template <uint32_t FT>
-RT_D int trav_steps_qspec(const DevScene& sc, const TravStack& stack, f3 o, f3 d, float time,
-                          float tmin, Trav& tr, int budget) {
-  uint32_t cur = tr.cur, pend = tr.top;
-  int sp = tr.sp;
-  const f3 inv = tr.inv;
-  int n = 0;
-  for (; n < budget && (cur != TRAV_DONE || pend != TRAV_DONE); ++n) {
-    if (cur != TRAV_DONE && (cur & LEAF_BIT) && pend == TRAV_DONE) {
-      pend = cur;
-      cur = sp == 0 ? TRAV_DONE : stack.pop(--sp);
-    }
-    const bool searching = pend == TRAV_DONE && cur != TRAV_DONE;
-    if (__any(searching)) {
-      if (cur == TRAV_DONE || (cur & LEAF_BIT)) continue;  // a parked leaf and a leaf next
-      const F4* it = (const F4*)((const char*)sc.nodes + (cur << 6));
-      F4 v[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = ld_glb(it + e);
-      float tn[4];
-      uint32_t ch[4];
-      qnode_children(v, o, inv, tmin, tr.best.t, tn, ch);
-      if (tn[0] != kInf) {
-        if (sp + 3 <= stack.nshort) {
-          lds_u32* q = (lds_u32*)stack.lds;
-          q[sp * 256] = ch[3];
-          sp += tn[3] != kInf;
-          q[sp * 256] = ch[2];
-          sp += tn[2] != kInf;
-          q[sp * 256] = ch[1];
-          sp += tn[1] != kInf;
-        } else {
-          if (tn[3] != kInf && sp < kStack) stack.push(sp++, ch[3]);
-          if (tn[2] != kInf && sp < kStack) stack.push(sp++, ch[2]);
-          if (tn[1] != kInf && sp < kStack) stack.push(sp++, ch[1]);
-        }
-        cur = ch[0];
-      } else {
-        cur = sp == 0 ? TRAV_DONE : stack.pop(--sp);
-      }
-    } else if (pend != TRAV_DONE) {
-      const F4* it = (const F4*)((const char*)sc.nodes + ((pend & 0x0FFFFFFFu) << 6));
-      F4 v[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = ld_glb(it + e);
-      float t, u, vv;
-      uint32_t ref;
-      const uint32_t rej = hit_record_m<FT>(v, o, d, inv.y, time, tmin, tr.best.t, t, u, vv, ref);
-      take_hit(tr, rej, t, u, vv, ref);
-      pend = TRAV_DONE;
-    }
-  }
-  // a budget cut with only a parked leaf left: hand it back as the current item (the next
-  // call parks it again), so "cur == TRAV_DONE" keeps meaning "traversal finished"
-  if (cur == TRAV_DONE && pend != TRAV_DONE) {
-    cur = pend;
-    pend = TRAV_DONE;
-  }
-  tr.cur = cur;
-  tr.sp = sp;
-  tr.top = pend;
-  return n;
-}
-#endif
 
 // QN: the compressed BVH4 (host_qbvh.cpp, rt_device.h "compressed BVH4 node"), 64-B
 // items read through L1/L2; cur = item index, LEAF_BIT set for a single-prim leaf record
@@ -663,14 +578,10 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
         float t, u, vv;
         uint32_t ref;
         const uint32_t rej = hit_record_m<FT>(v, o, d, inv.y, time, tmin, tr.best.t, t, u, vv, ref);
-#ifdef RT_QSPEC
-        take_hit(tr, rej, t, u, vv, ref);
-#else
         tr.best.t = bitsf(pick_by(fbits(t), fbits(tr.best.t), rej));
         tr.best.u = bitsf(pick_by(fbits(u), fbits(tr.best.u), rej));
         tr.best.v = bitsf(pick_by(fbits(vv), fbits(tr.best.v), rej));
         tr.best.ref = pick_by(ref, tr.best.ref, rej);
-#endif
       }
       if (sp == 0) cur = TRAV_DONE;
       else cur = stack.pop(--sp);
@@ -780,14 +691,10 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
           float t, u, vv;
           uint32_t ref;
           const uint32_t rej = hit_record_m<FT>(rec, o, d, inv.y, time, tmin, tr.best.t, t, u, vv, ref);
-#ifdef RT_QSPEC
-          take_hit(tr, rej, t, u, vv, ref);
-#else
           tr.best.t = bitsf(pick_by(fbits(t), fbits(tr.best.t), rej));
           tr.best.u = bitsf(pick_by(fbits(u), fbits(tr.best.u), rej));
           tr.best.v = bitsf(pick_by(fbits(vv), fbits(tr.best.v), rej));
           tr.best.ref = pick_by(ref, tr.best.ref, rej);
-#endif
           if (++k >= count) break;
           const F4* q = sc.leafprims + 4 * (size_t)(first + k);
           for (int e = 0; e < 4; ++e) rec[e] = ld_glb(q + e);
