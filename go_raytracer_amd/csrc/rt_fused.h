@@ -156,6 +156,7 @@ constexpr unsigned fused_static_lds(uint32_t ft, int tree = 4) {
 __shared__ unsigned long long g_tstart[4];  // per wave: k_fused's start time (RT_WAVE_TIMES)
 #ifdef RT_DRAIN_TIMES
 __shared__ unsigned long long g_tdrain[4];  // debug builds: when the wave's grab came back empty
+__shared__ unsigned long long g_dinfo[4][3];  // ... and then: samples left, busy lanes, segments
 #endif
 // TREE: 4 = BVH4, 5 = compressed BVH4 (64-B nodes, global only), 2 = BVH2, 0 = no tree
 // (every record tested, tiny scenes)
@@ -229,8 +230,25 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
     }
     PH_ADD(PH_GRAB, t_grab);
 #ifdef RT_DRAIN_TIMES
-    if (b.part >= (uint32_t)kMaxParts && lane_id() == 0u && g_tdrain[wave_in_group] == 0ull)
-      g_tdrain[wave_in_group] = wall_clock64();
+    if (b.part >= (uint32_t)kMaxParts && __builtin_amdgcn_readfirstlane((uint32_t)(g_tdrain[wave_in_group] != 0ull)) == 0u) {
+      uint32_t rem = has ? (s.flags >> kCountShift) - s.j : 0u, act = has ? 1u : 0u;
+#ifndef RT_WAVE_SEGS
+      uint32_t sg = s.segs;
+#else
+      uint32_t sg = 0u;
+#endif
+      for (int off = 32; off > 0; off >>= 1) {
+        rem += __shfl_xor(rem, off);
+        act += __shfl_xor(act, off);
+        sg += __shfl_xor(sg, off);
+      }
+      if (lane_id() == 0u) {
+        g_tdrain[wave_in_group] = wall_clock64();
+        g_dinfo[wave_in_group][0] = rem;
+        g_dinfo[wave_in_group][1] = act;
+        g_dinfo[wave_in_group][2] = sg;
+      }
+    }
 #endif
     if (!__any(has)) break;
     PH_T(t_trav);
@@ -312,6 +330,9 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
       for (int i = 0; i < PH_N; ++i) rec[4 + i] = g_ph[wave_in_group][i];
 #else
       for (int i = 0; i < PH_N; ++i) rec[4 + i] = 0ull;
+#ifdef RT_DRAIN_TIMES
+      for (int i = 0; i < 3; ++i) rec[4 + i] = g_dinfo[wave_in_group][i];
+#endif
 #endif
     }
   }

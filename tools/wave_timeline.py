@@ -47,6 +47,16 @@ with rt.Scene(t, w, l) as sc:
                 "drain_p50_by_dispatch_round_us": {
                     int(r): round(float(np.percentile(dr[(np.arange(len(a)) // 4 // 256) % max(len(a) // 4 // 256, 1) == r], 50)), 1)
                     for r in range(max(len(a) // 4 // 256, 1))}}), flush=True)
+            rem, act, segs_after = a[:, 4], a[:, 5], a[:, 2] - a[:, 6]
+            print(json.dumps({
+                "nranks": n, "left_at_drain_p50": q(rem, 50), "left_at_drain_p99": q(rem, 99),
+                "busy_lanes_at_drain_p50": q(act, 50),
+                "segments_after_drain_p50": q(segs_after, 50), "segments_after_drain_p99": q(segs_after, 99),
+                "corr_after_drain_time_vs_left": round(float(np.corrcoef(left, rem)[0, 1]), 3),
+                "corr_after_drain_time_vs_segments": round(float(np.corrcoef(left, segs_after)[0, 1]), 3),
+                "after_drain_us_by_left_quartile": [round(float(np.median(left[(rem >= lo) & (rem <= hi)])), 1)
+                    for lo, hi in zip(np.percentile(rem, [0, 25, 50, 75]), np.percentile(rem, [25, 50, 75, 100]))]}),
+                  flush=True)
         # end times by XCD (workgroups are dispatched round-robin: block % 8) and by the
         # wave's slot in its workgroup (one workgroup per CU slot: its 4 waves, one per SIMD)
         blk = np.arange(len(a)) // 4
