@@ -194,6 +194,9 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
   tr.cur = TRAV_DONE;
   bool has = false;
   WaveBatch b = batch_init(P);
+#ifdef RT_GQUEUE
+  bool gave = false;  // wave-uniform: this wave gave its lanes' spare samples to the queue
+#endif
   // debug (RT_WAVE_TIMES): the wave's start time parks in LDS (a register held across the
   // loop for this was the record-loop kernel's one spilled VGPR)
   // (the record-loop kernel keeps the wave's index in an SGPR: threadIdx.x >> 6 kept to the
@@ -220,7 +223,12 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
     // kernel only)
     constexpr bool kSplit = (FT == 0u && TREE == 0) || kSplitTrees;
     if constexpr (kSplit)
-      if (b.part >= (uint32_t)kMaxParts) split_samples(P, s, has, c, j0, n0);
+      if (b.part >= (uint32_t)kMaxParts) {
+        split_samples(P, s, has, c, j0, n0);
+#ifdef RT_GQUEUE
+        if constexpr (FT == 0u && TREE == 0) gqueue_step(s, has, c, j0, n0, gave);
+#endif
+      }
     if (c != 0xFFFFFFFFu) {
       start_sample<false, cam_mode(FT), FT == 0u && TREE == 0>(P, slot, s, c, j0);
       if constexpr (kSplit)
@@ -250,7 +258,13 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
       }
     }
 #endif
-    if (!__any(has)) break;
+    if (!__any(has)) {
+#ifdef RT_GQUEUE
+      if constexpr (FT == 0u && TREE == 0)
+        if (gqueue_pending()) continue;  // entries left: take them before ending
+#endif
+      break;
+    }
     PH_T(t_trav);
     if (has && tr.cur != TRAV_DONE)
     {

@@ -41,7 +41,8 @@ struct Counters {
   unsigned long long pushes;
   unsigned long long overflow;  // samples whose channel left the fixed-point range (add_sample)
   uint32_t chunk_head;
-  uint32_t _pad[11];
+  uint32_t gq_tail, gq_head;  // (RT_GQUEUE builds) the drain's device-wide queue of sample ranges
+  uint32_t _pad[9];
   uint32_t part[kMaxParts * kPartStride];  // fused kernel: next position of partition p at [p * stride]
   uint32_t cnt[kMaxIt][kXcd];  // per-XCD queue lengths entering iteration i
 };
@@ -2303,6 +2304,85 @@ RT_D void split_samples(const Params& P, Path& s, bool has, uint32_t& c, uint32_
     n0 = t_cnt;
   }
 }
+
+#ifdef RT_GQUEUE
+// Drain sharing across the whole device (record-loop kernel, RT_GQUEUE builds).  When a wave
+// first finds the chunk pool empty, each of its lanes with >= 2 samples left after the
+// current one gives the upper half of them to a device-wide queue: one 64-bit entry
+// (chunk:32 | ready:1 | end:12 | first:12) in the traversal-stack overflow buffer (unused by
+// the record loop, zeroed per launch), slots claimed with one atomic per wave on
+// Counters::gq_tail.  A wave whose lanes still need work after split_samples claims up to
+// that many entries with one compare-and-swap on gq_head and waits for each claimed slot's
+// ready bit (its pusher writes it right after its own atomic).  Each wave gives once, so the
+// queue holds at most one entry per lane.  A wave ends only once the queue is empty, so every
+// entry is taken by some wave: its pusher at the latest.  Taken samples go to the pixel with
+// atomics (F_SPLIT), as with split_samples.
+RT_D void gqueue_step(Path& s, bool has, uint32_t& c, uint32_t& j0, uint32_t& n0, bool& gave) {
+  const cst_params* kp = kparams();
+  unsigned long long* q = (unsigned long long*)kp->ostack;
+  uint32_t* tail = &kp->ctr->gq_tail;
+  uint32_t* head = &kp->ctr->gq_head;
+  const uint32_t lane = lane_id();
+  if (!gave) {
+    gave = true;
+    const uint32_t cnt = s.flags >> kCountShift;
+    const uint32_t left = has ? cnt - 1u - s.j : 0u;
+    const bool give = left >= 2u;
+    const unsigned long long m = __ballot(give);
+    if (m) {
+      const uint32_t leader = (uint32_t)(__ffsll((long long)m) - 1);
+      uint32_t base = 0u;
+      if (lane == leader) base = atomicAdd(tail, (uint32_t)__popcll(m));
+      base = __builtin_amdgcn_readlane(base, leader);
+      if (give) {
+        const uint32_t keep = cnt - (left >> 1);  // the giver keeps [.., keep)
+        const unsigned long long e = ((unsigned long long)s.chunk << 32) | 0x80000000ull |
+                                     ((unsigned long long)cnt << 12) | keep;
+        __hip_atomic_store(&q[base + prefix_count(m)], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s.flags = (s.flags & ((1u << kCountShift) - 1u)) | (keep << kCountShift);
+      }
+    }
+  }
+  const bool needs = !has && c == 0xFFFFFFFFu;
+  const unsigned long long need = __ballot(needs);
+  if (!need) return;
+  const uint32_t leader = (uint32_t)(__ffsll((long long)need) - 1);
+  uint32_t h = 0u, k = 0u;
+  if (lane == leader) {
+    const uint32_t t = __hip_atomic_load(tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    h = __hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (h < t) {
+      k = min((uint32_t)__popcll(need), t - h);
+      uint32_t exp = h;
+      if (!__hip_atomic_compare_exchange_strong(head, &exp, h + k, __ATOMIC_RELAXED,
+                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        k = 0u;
+    }
+  }
+  h = __builtin_amdgcn_readlane(h, leader);
+  k = __builtin_amdgcn_readlane(k, leader);
+  const uint32_t r = prefix_count(need);
+  if (needs && r < k) {
+    unsigned long long e;
+    while (!((e = __hip_atomic_load(&q[h + r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) &
+             0x80000000ull))
+      __builtin_amdgcn_s_sleep(1);
+    c = (uint32_t)(e >> 32);
+    j0 = (uint32_t)e & 0xFFFu;
+    n0 = ((uint32_t)e >> 12) & 0xFFFu;
+  }
+}
+// the queue still holds entries nobody has claimed (wave-uniform)
+RT_D bool gqueue_pending() {
+  const cst_params* kp = kparams();
+  uint32_t t = 0u, h = 0u;
+  if (lane_id() == 0u) {
+    t = __hip_atomic_load(&kp->ctr->gq_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    h = __hip_atomic_load(&kp->ctr->gq_head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return __builtin_amdgcn_readfirstlane(h < t ? 1u : 0u) != 0u;
+}
+#endif
 
 // Wave-batched work distribution over partitioned counters.  The chunk range is split
 // into NP = 2^parts_log2 partitions, interleaved in granules of G = 2^gran_log2 chunks
