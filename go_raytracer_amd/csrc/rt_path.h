@@ -2338,7 +2338,9 @@ RT_D void gqueue_step(Path& s, bool has, uint32_t& c, uint32_t& j0, uint32_t& n0
         const uint32_t keep = cnt - (left >> 1);  // the giver keeps [.., keep)
         const unsigned long long e = ((unsigned long long)s.chunk << 32) | 0x80000000ull |
                                      ((unsigned long long)cnt << 12) | keep;
-        __hip_atomic_store(&q[base + prefix_count(m)], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // (read-modify-write atomics throughout: they are performed where every XCD sees
+        // them, while a plain or atomic load may return a value cached in this XCD's L2)
+        atomicExch(&q[base + prefix_count(m)], e);
         s.flags = (s.flags & ((1u << kCountShift) - 1u)) | (keep << kCountShift);
       }
     }
@@ -2349,8 +2351,8 @@ RT_D void gqueue_step(Path& s, bool has, uint32_t& c, uint32_t& j0, uint32_t& n0
   const uint32_t leader = (uint32_t)(__ffsll((long long)need) - 1);
   uint32_t h = 0u, k = 0u;
   if (lane == leader) {
-    const uint32_t t = __hip_atomic_load(tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    h = __hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t t = atomicAdd(tail, 0u);
+    h = atomicAdd(head, 0u);
     if (h < t) {
       k = min((uint32_t)__popcll(need), t - h);
       uint32_t exp = h;
@@ -2364,9 +2366,7 @@ RT_D void gqueue_step(Path& s, bool has, uint32_t& c, uint32_t& j0, uint32_t& n0
   const uint32_t r = prefix_count(need);
   if (needs && r < k) {
     unsigned long long e;
-    while (!((e = __hip_atomic_load(&q[h + r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) &
-             0x80000000ull))
-      __builtin_amdgcn_s_sleep(1);
+    while (!((e = atomicAdd(&q[h + r], 0ull)) & 0x80000000ull)) __builtin_amdgcn_s_sleep(1);
     c = (uint32_t)(e >> 32);
     j0 = (uint32_t)e & 0xFFFu;
     n0 = ((uint32_t)e >> 12) & 0xFFFu;
@@ -2377,8 +2377,8 @@ RT_D bool gqueue_pending() {
   const cst_params* kp = kparams();
   uint32_t t = 0u, h = 0u;
   if (lane_id() == 0u) {
-    t = __hip_atomic_load(&kp->ctr->gq_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    h = __hip_atomic_load(&kp->ctr->gq_head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    t = atomicAdd(&kp->ctr->gq_tail, 0u);
+    h = atomicAdd(&kp->ctr->gq_head, 0u);
   }
   return __builtin_amdgcn_readfirstlane(h < t ? 1u : 0u) != 0u;
 }

@@ -1044,8 +1044,12 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   if (o.chunk > 0) {
     K = (uint32_t)o.chunk;
   } else if (mode == RT_MODE_FUSED) {
+    // (the mesh set asks 200: the 1M-triangle mesh's 2- / 4- / 8-GPU shares -0.6 / -1.6 /
+    // -2.3 % with K halved, its whole image unchanged at K = 32; book1 and book2 gained
+    // nothing from it, profiles/r5_model_chunk_share_ab.jsonl, r5_chunk_need200_ab.jsonl)
+    const int need_dflt = f_lds ? 12 : ft_set == (FT_SPHERE | FT_TRI | FT_METAL) ? 200 : 100;
     const uint64_t work = (uint64_t)npix * ss,
-                   need = (uint64_t)std::max(1, env_int("RT_CHUNK_NEED", f_lds ? 12 : 100)) * P;
+                   need = (uint64_t)std::max(1, env_int("RT_CHUNK_NEED", need_dflt)) * P;
     K = f_lds ? 8u : 4u;  // the smallest: C3's 8-GPU share 6 % faster at 4 than 8 (C2's ±1 %)
     for (uint32_t k : {32u, 16u, 8u})
       if (work / k >= need) {
