@@ -427,6 +427,17 @@ class Scene:
                                          refs.ctypes.data or None, C.byref(nr)))
         return nodes, refs
 
+    def export_qbvh(self):
+        """(items uint32 [N, 16]: the compressed BVH4's 64-B items, nodes4 uint32 [M, 32]:
+        the BVH4 they encode, root4) -- rt_device.h layouts, for structural tests."""
+        ni, nn, root = C.c_int32(), C.c_int32(), C.c_uint32()
+        check(lib().rt_scene_export_qbvh(self._p, None, C.byref(ni), None, C.byref(nn), C.byref(root)))
+        items = np.zeros((max(ni.value, 0), 16), np.uint32)
+        nodes = np.zeros((max(nn.value, 0), 32), np.uint32)
+        check(lib().rt_scene_export_qbvh(self._p, items.ctypes.data or None, C.byref(ni),
+                                         nodes.ctypes.data or None, C.byref(nn), C.byref(root)))
+        return items, nodes, int(root.value)
+
     MODES = {"auto": 0, "wavefront": 1, "fused": 2}
 
     @staticmethod

@@ -181,6 +181,8 @@ SIGNATURES = {
                                  C.POINTER(C.c_int32), C.POINTER(C.c_uint32)]),
     "rt_scene_export_bvh8": (_I, [_P, C.c_void_p, C.POINTER(C.c_int32), C.c_void_p,
                                   C.POINTER(C.c_int32)]),
+    "rt_scene_export_qbvh": (_I, [_P, C.c_void_p, C.POINTER(C.c_int32), C.c_void_p,
+                                  C.POINTER(C.c_int32), C.POINTER(C.c_uint32)]),
     "rt_scene_export_prim_bounds": (_I, [_P, C.c_void_p, C.POINTER(C.c_int32)]),
     "rt_render": (_I, [_P, C.POINTER(RtCamera), C.POINTER(RtRenderOpts), C.c_void_p,
                        C.POINTER(RtStats)]),

@@ -195,7 +195,7 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
   bool has = false;
   WaveBatch b = batch_init(P);
 #ifdef RT_GQUEUE
-  bool gave = false;  // wave-uniform: this wave gave its lanes' spare samples to the queue
+  GQueue gq = {false, 0u, 0u};
 #endif
   // debug (RT_WAVE_TIMES): the wave's start time parks in LDS (a register held across the
   // loop for this was the record-loop kernel's one spilled VGPR)
@@ -226,7 +226,7 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
       if (b.part >= (uint32_t)kMaxParts) {
         split_samples(P, s, has, c, j0, n0);
 #ifdef RT_GQUEUE
-        if constexpr (FT == 0u && TREE == 0) gqueue_step(s, has, c, j0, n0, gave);
+        if constexpr (FT == 0u && TREE == 0) gqueue_step(s, has, c, j0, n0, gq);
 #endif
       }
     if (c != 0xFFFFFFFFu) {
@@ -260,8 +260,18 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
 #endif
     if (!__any(has)) {
 #ifdef RT_GQUEUE
-      if constexpr (FT == 0u && TREE == 0)
-        if (gqueue_pending()) continue;  // entries left: take them before ending
+      // a wave that pushed runs whatever of its own block nobody took before it ends
+      if constexpr (FT == 0u && TREE == 0) {
+        if (gqueue_sweep(c, j0, n0, gq)) {
+          if (c != 0xFFFFFFFFu) {
+            start_sample<false, cam_mode(FT), FT == 0u && TREE == 0>(P, slot, s, c, j0);
+            s.flags = F_SPLIT | (n0 << kCountShift);
+            trav_init<FT>(P.sc, s.o, s.d, s.time, tr);
+            has = true;
+          }
+          continue;
+        }
+      }
 #endif
       break;
     }

@@ -1778,4 +1778,21 @@ int rt_device_count(void) {
   return n;
 }
 
+int rt_scene_export_qbvh(const rt_scene* sc, float* items, int32_t* n_items, float* nodes4,
+                         int32_t* n_nodes4, uint32_t* root4) {
+  if (!sc) return rt::set_error(RT_ERR_INVALID, "rt_scene_export_qbvh: null");
+  const rt::HostScene& h = sc->s.h;
+  std::vector<rt::F4> recs, qb;
+  rt::build_leaf_records(h, recs);
+  size_t n = 0;
+  const int rc = rt::build_qbvh(h, recs, &qb, &n);
+  if (rc != RT_OK) return rc;
+  if (n_items) *n_items = (int32_t)n;
+  if (n_nodes4) *n_nodes4 = (int32_t)(h.nodes4.size() / 8);
+  if (root4) *root4 = h.root4;
+  if (items && n) memcpy(items, qb.data(), n * 64);
+  if (nodes4 && !h.nodes4.empty()) memcpy(nodes4, h.nodes4.data(), h.nodes4.size() * 16);
+  return RT_OK;
+}
+
 }  // extern "C"

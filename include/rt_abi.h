@@ -319,6 +319,12 @@ int rt_scene_export_bvh8(const rt_scene* s, float* nodes, int32_t* n_nodes, uint
                          int32_t* n_refs8);
 /* world-prim float AABBs in prim-ref order (6 floats each) */
 int rt_scene_export_prim_bounds(const rt_scene* s, float* bounds, int32_t* n);
+/* the compressed BVH4 the fused kernels read through L1/L2 (rt_device.h "compressed BVH4
+ * node", 64-B items: nodes with fp16 child planes and single-prim leaf records; 0 items when
+ * the scene's tree is not encodable) and the BVH4 it encodes (8 float4 per node), for
+ * structural tests.  NULL pointers query the counts. */
+int rt_scene_export_qbvh(const rt_scene* s, float* items, int32_t* n_items, float* nodes4,
+                         int32_t* n_nodes4, uint32_t* root4);
 
 enum {
   RT_FLAG_PROFILE = 1,     /* time every kernel with HIP events */

@@ -240,3 +240,78 @@ def test_box_leaves_kept_only_where_they_pay(rt, tune):
     t, cam, w, l = scenes.boxes(rt)  # 216 quads, lean set: expanded
     with rt.Scene(t, w, l) as sc:
         assert not sc.info()["features"] & rt.RT_FT_BOX
+
+
+def qbvh_invariants(sc):
+    """host_qbvh.cpp: the compressed BVH4 mirrors the BVH4 item by item -- every BVH4 node
+    is one 64-B node item, every single-prim leaf one leaf record (its bit set in the node's
+    leaf mask), every 2-4-prim leaf one node over its prims -- and every child box it encodes
+    (fp32 corner + fp16 offsets, exact in float64) contains the fp32 box it replaces, so the
+    traversal culls no more than the BVH4's (the images are bit-identical on the GPU,
+    test_compressed_bvh_renders_like_bvh4).  Empty slots decode to inverted infinite boxes."""
+    items, nodes4, root4 = sc.export_qbvh()
+    _, refs, _, bounds = sc.export_bvh()
+    assert len(items) > 0 and len(nodes4) > 0
+    LEAF, EMPTY = 0x80000000, 0xFFFFFFFE
+
+    def planes(item):
+        w = items[item]
+        corner = w[0:3].view(np.float32).astype(np.float64)
+        half = w[4:16].view(np.float16).astype(np.float64).reshape(3, 4, 2)  # [axis][word][half]
+        lo = np.stack([half[:, 0, 0], half[:, 0, 1], half[:, 1, 0], half[:, 1, 1]], 1)  # [axis][k]
+        hi = np.stack([half[:, 2, 0], half[:, 2, 1], half[:, 3, 0], half[:, 3, 1]], 1)
+        return corner, lo, hi, int(w[3]) & 0x0FFFFFFF, int(w[3]) >> 28
+
+    seen_nodes = np.zeros(len(nodes4), np.int32)
+    seen_refs = np.zeros(len(refs), np.int32)
+    used = np.zeros(len(items), np.int32)
+    used[0] = 1
+    stack = [(0, ("node", root4))]
+    while stack:
+        item, (kind, what) = stack.pop()
+        corner, lo, hi, base, lmask = planes(item)
+        if kind == "node":
+            seen_nodes[what] += 1
+            nd = nodes4[what].view(np.float32).reshape(8, 4)  # [field][child]
+            codes = nodes4[what][0:4]
+            kids = []
+            for k in range(4):
+                c = int(codes[k])
+                blo = np.array([nd[1 + 2 * a, k] for a in range(3)], np.float64)
+                bhi = np.array([nd[2 + 2 * a, k] for a in range(3)], np.float64)
+                if c == EMPTY or not (blo <= bhi).all():
+                    kids.append(None)
+                elif c & LEAF:
+                    first, count = (c >> 4) & 0x7FFFFFF, (c & 15) + 1
+                    kids.append((blo, bhi, ("leaf", first) if count == 1 else ("group", (first, count))))
+                else:
+                    kids.append((blo, bhi, ("node", c)))
+        else:  # a node over the prims of one 2-4-prim BVH4 leaf
+            first, count = what
+            kids = [(bounds[first + k][:3].astype(np.float64), bounds[first + k][3:].astype(np.float64),
+                     ("leaf", first + k)) if k < count else None for k in range(4)]
+        for k, kid in enumerate(kids):
+            if kid is None:
+                assert (lo[:, k] == np.inf).all() and (hi[:, k] == -np.inf).all(), (item, k)
+                used[base + k] += 1  # its (unused) slot of the node's four
+                continue
+            blo, bhi, nxt = kid
+            assert (corner + lo[:, k] <= blo).all() and (corner + hi[:, k] >= bhi).all(), (item, k)
+            child = base + k
+            used[child] += 1
+            if nxt[0] == "leaf":
+                assert (lmask >> k) & 1, (item, k)
+                seen_refs[nxt[1]] += 1
+            else:
+                assert not (lmask >> k) & 1, (item, k)
+                stack.append((child, nxt))
+    assert (seen_nodes == 1).all(), "every BVH4 node is encoded exactly once"
+    assert (seen_refs == 1).all(), "every prim has exactly one leaf record"
+    assert (used == 1).all(), "every item is one node's child slot, exactly once"
+
+
+@pytest.mark.parametrize("name", ["book1", "book2", "model:96x24", "model:256x32"])
+def test_qbvh_invariants(rt, name):
+    t, cam, w, l = rt.demo_scene(name)
+    with rt.Scene(t, w, l) as sc:
+        qbvh_invariants(sc)
