@@ -194,9 +194,6 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
   tr.cur = TRAV_DONE;
   bool has = false;
   WaveBatch b = batch_init(P);
-#ifdef RT_GQUEUE
-  GQueue gq = {false, 0u, 0u};
-#endif
   // debug (RT_WAVE_TIMES): the wave's start time parks in LDS (a register held across the
   // loop for this was the record-loop kernel's one spilled VGPR)
   // (the record-loop kernel keeps the wave's index in an SGPR: threadIdx.x >> 6 kept to the
@@ -223,12 +220,7 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
     // kernel only)
     constexpr bool kSplit = (FT == 0u && TREE == 0) || kSplitTrees;
     if constexpr (kSplit)
-      if (b.part >= (uint32_t)kMaxParts) {
-        split_samples(P, s, has, c, j0, n0);
-#ifdef RT_GQUEUE
-        if constexpr (FT == 0u && TREE == 0) gqueue_step(s, has, c, j0, n0, gq);
-#endif
-      }
+      if (b.part >= (uint32_t)kMaxParts) split_samples(P, s, has, c, j0, n0);
     if (c != 0xFFFFFFFFu) {
       start_sample<false, cam_mode(FT), FT == 0u && TREE == 0>(P, slot, s, c, j0);
       if constexpr (kSplit)
@@ -258,23 +250,7 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
       }
     }
 #endif
-    if (!__any(has)) {
-#ifdef RT_GQUEUE
-      // a wave that pushed runs whatever of its own block nobody took before it ends
-      if constexpr (FT == 0u && TREE == 0) {
-        if (gqueue_sweep(c, j0, n0, gq)) {
-          if (c != 0xFFFFFFFFu) {
-            start_sample<false, cam_mode(FT), FT == 0u && TREE == 0>(P, slot, s, c, j0);
-            s.flags = F_SPLIT | (n0 << kCountShift);
-            trav_init<FT>(P.sc, s.o, s.d, s.time, tr);
-            has = true;
-          }
-          continue;
-        }
-      }
-#endif
-      break;
-    }
+    if (!__any(has)) break;
     PH_T(t_trav);
     if (has && tr.cur != TRAV_DONE)
     {
@@ -366,6 +342,13 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
 // iterative-ILP machine scheduler (Makefile): the C5 mesh set and the C3 sphere set
 // (C5 -0.6 / -1.0 %, C3 -0.8 %, images bit-identical; the same strategy costs the C2 kernel
 // 3.5 %, profiles/r3_sched_strategy_ab.jsonl, r3_split_ilp_ab.jsonl).  X(LDS, FT, TREE).
+#ifdef RT_Q_DEFAULT_SCHED
+#define RT_FUSED_ILP_KERNELS(X)                                             \
+  X(true, (FT_SPHERE | FT_TRI | FT_METAL), 4)                               \
+  X(false, (FT_SPHERE | FT_TRI | FT_METAL), 4)                              \
+  X(true, (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER), 4)        \
+  X(false, (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER), 4)
+#else
 #define RT_FUSED_ILP_KERNELS(X)                                             \
   X(true, (FT_SPHERE | FT_TRI | FT_METAL), 4)                               \
   X(false, (FT_SPHERE | FT_TRI | FT_METAL), 4)                              \
@@ -373,5 +356,6 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
   X(false, (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER), 4)       \
   X(false, (FT_SPHERE | FT_TRI | FT_METAL), 5)                              \
   X(false, (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER), 5)
+#endif
 
 }  // namespace rt

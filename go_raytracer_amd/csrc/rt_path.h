@@ -41,8 +41,7 @@ struct Counters {
   unsigned long long pushes;
   unsigned long long overflow;  // samples whose channel left the fixed-point range (add_sample)
   uint32_t chunk_head;
-  uint32_t gq_tail, gq_head;  // (RT_GQUEUE builds) the drain's device-wide queue of sample ranges
-  uint32_t _pad[9];
+  uint32_t _pad[11];
   uint32_t part[kMaxParts * kPartStride];  // fused kernel: next position of partition p at [p * stride]
   uint32_t cnt[kMaxIt][kXcd];  // per-XCD queue lengths entering iteration i
 };
@@ -2304,93 +2303,6 @@ RT_D void split_samples(const Params& P, Path& s, bool has, uint32_t& c, uint32_
     n0 = t_cnt;
   }
 }
-
-#ifdef RT_GQUEUE
-// Drain sharing across the whole device (record-loop kernel, RT_GQUEUE builds).  When a wave
-// first finds the chunk pool empty, each of its lanes with >= 2 samples left after the
-// current one gives the upper half of them to a device-wide queue: one 64-bit entry
-// (chunk:32 | ready:1 | end:12 | first:12) in the traversal-stack overflow buffer (unused by
-// the record loop, zeroed per launch), a block of slots claimed with one atomic per wave on
-// Counters::gq_tail.  Lanes still idle after split_samples claim a block of slots with one
-// compare-and-swap on gq_head (after a plain, possibly stale look: thousands of waves
-// polling one address with returning atomics would serialise on it) and take each entry
-// with an atomic exchange against 0.  An entry is consumed exactly once, by whichever
-// exchange sees it written: a taker that reaches its slot before the pusher wrote it gets 0
-// and nothing, and the pushing wave sweeps its own slots with the same exchange when its
-// lanes run out of work, so every entry is run.  No wave waits on another.  Taken samples go
-// to the pixel with atomics (F_SPLIT), as with split_samples.
-struct GQueue {
-  bool gave;       // wave-uniform: the wave has passed its first drain round
-  uint32_t base;   // wave-uniform: its block of slots [base, base + count)
-  uint32_t count;  // (0: it pushed nothing, or has swept its block)
-};
-RT_D void gq_take(unsigned long long e, uint32_t& c, uint32_t& j0, uint32_t& n0) {
-  c = (uint32_t)(e >> 32);
-  j0 = (uint32_t)e & 0xFFFu;
-  n0 = ((uint32_t)e >> 12) & 0xFFFu;
-}
-RT_D void gqueue_step(Path& s, bool has, uint32_t& c, uint32_t& j0, uint32_t& n0, GQueue& g) {
-  const cst_params* kp = kparams();
-  if (kp->split_min == 0u) return;  // RT_SPLIT_MIN=0: no drain sharing at all
-  unsigned long long* q = (unsigned long long*)kp->ostack;
-  uint32_t* tail = &kp->ctr->gq_tail;
-  const uint32_t lane = lane_id();
-  if (!g.gave) {
-    g.gave = true;
-    const uint32_t cnt = s.flags >> kCountShift;
-    const uint32_t left = has ? cnt - 1u - s.j : 0u;
-    const bool give = left >= 2u;
-    const unsigned long long m = __ballot(give);
-    if (m) {
-      const uint32_t leader = (uint32_t)(__ffsll((long long)m) - 1);
-      uint32_t base = 0u;
-      if (lane == leader) base = atomicAdd(tail, (uint32_t)__popcll(m));
-      g.base = __builtin_amdgcn_readlane(base, leader);
-      g.count = (uint32_t)__popcll(m);
-      if (give) {
-        const uint32_t keep = cnt - (left >> 1);  // the giver keeps [.., keep)
-        const unsigned long long e = ((unsigned long long)s.chunk << 32) | 0x80000000ull |
-                                     ((unsigned long long)cnt << 12) | keep;
-        atomicExch(&q[g.base + prefix_count(m)], e);
-        s.flags = (s.flags & ((1u << kCountShift) - 1u)) | (keep << kCountShift);
-      }
-    }
-  }
-  const bool needs = !has && c == 0xFFFFFFFFu;
-  if (!__any(needs)) return;
-  // no shared head: each idle lane probes one slot below the (possibly stale) tail with an
-  // exchange -- returning atomics on distinct addresses, which do not serialise
-  uint32_t t = 0u;
-  if (lane == 0u) t = __hip_atomic_load(tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  t = __builtin_amdgcn_readfirstlane(t);
-  if (needs && t > 0u) {
-    uint32_t x = (s.gpix * 0x9E3779B1u) ^ (s.j * 0x85EBCA77u) ^ ((uint32_t)wall_clock64() * 0xC2B2AE3Du) ^ lane;
-    x ^= x >> 15;
-    x *= 0x2C1B3C6Du;
-    x ^= x >> 12;
-    const uint32_t slot = (uint32_t)(((unsigned long long)x * t) >> 32);
-    const unsigned long long e = atomicExch(&q[slot], 0ull);
-    if (e & 0x80000000ull) gq_take(e, c, j0, n0);
-  }
-}
-// A pushing wave whose lanes all ran out of work takes back what is left of its own block
-// (wave-uniform call; true when some lane got work)
-RT_D bool gqueue_sweep(uint32_t& c, uint32_t& j0, uint32_t& n0, GQueue& g) {
-  if (g.count == 0u) return false;
-  unsigned long long* q = (unsigned long long*)kparams()->ostack;
-  const uint32_t lane = lane_id();
-  bool got = false;
-  if (lane < g.count) {
-    const unsigned long long e = atomicExch(&q[g.base + lane], 0ull);
-    if (e & 0x80000000ull) {
-      gq_take(e, c, j0, n0);
-      got = true;
-    }
-  }
-  g.count = 0u;
-  return __any(got);
-}
-#endif
 
 // Wave-batched work distribution over partitioned counters.  The chunk range is split
 // into NP = 2^parts_log2 partitions, interleaved in granules of G = 2^gran_log2 chunks

@@ -1294,11 +1294,6 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   };
 
   HIP_OK(hipMemsetAsync(st->ctr, 0, sizeof(Counters), stream));
-#ifdef RT_GQUEUE
-  // the record loop's drain queue lives in the (then unused) traversal-stack overflow buffer
-  if (mode == RT_MODE_FUSED && tree == 0 && ft_set == 0u)
-    HIP_OK(hipMemsetAsync(st->ostack, 0, (size_t)P * sizeof(unsigned long long), stream));
-#endif
   if (npix > 0) {
     HIP_OK(hipMemsetAsync(st->accum, 0, 3 * (size_t)npix * sizeof(unsigned long long), stream));
     HIP_OK(hipMemsetAsync(st->side, 0, 3 * (size_t)npix * sizeof(double), stream));
