@@ -63,8 +63,8 @@ RT_D void finish_hit(const Params& P, const Path& s, Hit& best) {
 #endif
 #ifndef TRI_QWAVES
 // the {sphere, triangle, metal} set (C5) on the compressed BVH4 at 5 waves per SIMD (round
-// 5): that kernel needs 113 VGPRs at 4, and 5 waves (96 VGPRs, 6 spilled; 12 LDS stack
-// entries, TRI_QSHORT, so five blocks fit the CU's LDS) measured C5 -3.8 %
+// 5): that kernel needs 113 VGPRs at 4, and 5 waves (96 VGPRs, 1 spilled with the default
+// scheduler; 12 LDS stack entries, TRI_QSHORT, so five blocks fit the CU's LDS) measured C5 -3.8 %
 // (profiles/r5_c4_c5_isolation_ab.jsonl); round 2's 5-wave try of the 128-B-node kernel
 // spilled 32 VGPRs in the traversal loop and lost 24 %
 #define TRI_QWAVES 5
@@ -73,9 +73,10 @@ RT_D void finish_hit(const Params& P, const Path& s, Hit& best) {
 #define TRI_QSHORT 12
 #endif
 #ifndef MESH_QWAVES
-// book1's set (C3) on the compressed BVH4 at 5 waves too (96 VGPRs, 26 spilled, 12 LDS stack
-// entries): C3 -1.2 % (profiles/r5_waves5_ab.jsonl); book2's set at 5 waves lost 3 % (31
-// spilled), it stays at 4
+// book1's set (C3) on the compressed BVH4 at 5 waves too (96 VGPRs, 2 spilled with the default
+// scheduler, 12 LDS stack entries): C3 -1.2 % with the ILP scheduler's 26 spills
+// (profiles/r5_waves5_ab.jsonl), -5.5 % more without them; book2's set at 5 waves lost 3 %
+// (31 spilled), it stays at 4
 #define MESH_QWAVES 5
 #endif
 #ifndef MESH_QSHORT
@@ -342,20 +343,13 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
 // iterative-ILP machine scheduler (Makefile): the C5 mesh set and the C3 sphere set
 // (C5 -0.6 / -1.0 %, C3 -0.8 %, images bit-identical; the same strategy costs the C2 kernel
 // 3.5 %, profiles/r3_sched_strategy_ab.jsonl, r3_split_ilp_ab.jsonl).  X(LDS, FT, TREE).
-#ifdef RT_Q_DEFAULT_SCHED
+// The compressed-BVH kernels (TREE 5) are not in this list: at 5 waves per SIMD the ILP
+// scheduler spilled 6 / 26 VGPRs in them against 1 / 2 with the default one, and the default
+// one renders C3 5.5 % and C5 0.3 % faster (bit-identical, profiles/r5_q_sched_ab.jsonl).
 #define RT_FUSED_ILP_KERNELS(X)                                             \
   X(true, (FT_SPHERE | FT_TRI | FT_METAL), 4)                               \
   X(false, (FT_SPHERE | FT_TRI | FT_METAL), 4)                              \
   X(true, (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER), 4)        \
   X(false, (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER), 4)
-#else
-#define RT_FUSED_ILP_KERNELS(X)                                             \
-  X(true, (FT_SPHERE | FT_TRI | FT_METAL), 4)                               \
-  X(false, (FT_SPHERE | FT_TRI | FT_METAL), 4)                              \
-  X(true, (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER), 4)        \
-  X(false, (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER), 4)       \
-  X(false, (FT_SPHERE | FT_TRI | FT_METAL), 5)                              \
-  X(false, (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER), 5)
-#endif
 
 }  // namespace rt
