@@ -346,6 +346,7 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
 // The compressed-BVH kernels (TREE 5) are not in this list: at 5 waves per SIMD the ILP
 // scheduler spilled 6 / 26 VGPRs in them against 1 / 2 with the default one, and the default
 // one renders C3 5.5 % and C5 0.3 % faster (bit-identical, profiles/r5_q_sched_ab.jsonl).
+// (book2's compressed-BVH kernel with the ILP scheduler: C4 +0.7 %, r5_book2_sched_ab.jsonl)
 #define RT_FUSED_ILP_KERNELS(X)                                             \
   X(true, (FT_SPHERE | FT_TRI | FT_METAL), 4)                               \
   X(false, (FT_SPHERE | FT_TRI | FT_METAL), 4)                              \
