@@ -212,14 +212,16 @@ def test_kernel_selection(rt, gpu, name, width, lean, width_tree, lds):
         assert st["lds_scene"] == lds
 
 
-@pytest.mark.parametrize("var", ["RT_BRUTE_AXIS", "RT_BRUTE_VERT"])
+@pytest.mark.parametrize("var", ["RT_BRUTE_AXIS", "RT_BRUTE_VERT", "RT_BRUTE_MIXED"])
 @pytest.mark.parametrize("name", ["cornell", "cornell_smoke"])
 def test_axis_record_groups_match_general_test(rt, gpu, tune, var, name):
-    """The record loop's axis-aligned groups (rt_path.h brute_axis) and its y-parallel
-    group (brute_vert: the rotated boxes' sides) compute the general quad test's t,
-    alpha and beta bit for bit: the Cornell boxes render the same image with either
-    grouping switched off (RT_BRUTE_AXIS=0 / RT_BRUTE_VERT=0).  The boxes' records stay
-    in the loop here (RT_BRUTE_BOX=0): the slab test is checked below."""
+    """The record loop's axis-aligned groups (rt_path.h brute_axis), its y-parallel
+    group (brute_vert: the rotated boxes' sides) and the mixed pair of two groups' odd
+    records (brute_mixed: the light on y and the back wall on z in Cornell) compute the
+    general quad test's t, alpha and beta bit for bit: the Cornell boxes render the same
+    image with each switched off (RT_BRUTE_AXIS=0 / RT_BRUTE_VERT=0 / RT_BRUTE_MIXED=0).
+    The boxes' records stay in the loop here (RT_BRUTE_BOX=0): the slab test is checked
+    below."""
     t, cam, w, l = rt.demo_scene(name)
     cam.Width, cam.SamplesPerPixel = 96, 64
     tune("RT_BRUTE_BOX", "0")
