@@ -1228,10 +1228,11 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   // Round 5, on the compressed BVH4 (cheaper node steps, 5 waves per SIMD): the mesh
   // scene is fastest at 5 steps and 32 ready lanes (C5 +4.6 % over 8 / 16 at 256 spp;
   // 64 ready lanes halves it), book2 unchanged at 8 / 32 (6 / 32 within 0.1 %), book1 at
-  // 12 / 1 (profiles/r5_sched_sweep_q.jsonl)
+  // 12 / 1 (profiles/r5_sched_sweep_q.jsonl) -- then 10 steps for book1: -0.7 % at full size
+  // (r5_c3_step_ab.jsonl; 9 to 16 swept at 256 spp, r5_knob_sweeps_q.jsonl)
   const bool big_tree = s->h.nodes4.size() / 8 >= 1024;
   const bool long_shade = ft_set == FT_ALL || (ft_set & FT_NOISE);
-  p.step_budget = env_int("RT_STEP_BUDGET", f_lds ? (1 << 30) : big_tree ? (long_shade ? 8 : 5) : 12);
+  p.step_budget = env_int("RT_STEP_BUDGET", f_lds ? (1 << 30) : big_tree ? (long_shade ? 8 : 5) : 10);
   p.shade_min = (uint32_t)env_int("RT_SHADE_MIN", f_lds ? 1 : (long_shade || big_tree) ? 32 : 1);
   // chunks per refill of a wave's batch (one returning atomic on the chunk
   // counter each): C2 grab sweep (profiles/r1_grab_sweep.jsonl) 64 -> 128:
