@@ -64,23 +64,25 @@ RT_D void finish_hit(const Params& P, const Path& s, Hit& best) {
 #ifndef TRI_QWAVES
 // the {sphere, triangle, metal} set (C5) on the compressed BVH4 at 5 waves per SIMD (round
 // 5): that kernel needs 113 VGPRs at 4, and 5 waves (96 VGPRs, 1 spilled with the default
-// scheduler; 12 LDS stack entries, TRI_QSHORT, so five blocks fit the CU's LDS) measured C5 -3.8 %
+// scheduler; 13 LDS stack entries, TRI_QSHORT, so five blocks fit the CU's LDS) measured C5 -3.8 %
 // (profiles/r5_c4_c5_isolation_ab.jsonl); round 2's 5-wave try of the 128-B-node kernel
 // spilled 32 VGPRs in the traversal loop and lost 24 %
 #define TRI_QWAVES 5
 #endif
 #ifndef TRI_QSHORT
-#define TRI_QSHORT 12
+// 13 LDS traversal-stack entries fill five blocks' LDS (5 x 31,776 B of 160 KiB): C5 -1.5 %,
+// C3 -0.3 % against 12, 10 +4.5 % (profiles/r5_qshort_ab.jsonl)
+#define TRI_QSHORT 13
 #endif
 #ifndef MESH_QWAVES
-// book1's set (C3) on the compressed BVH4 at 5 waves too (96 VGPRs, 2 spilled with the default
-// scheduler, 12 LDS stack entries): C3 -1.2 % with the ILP scheduler's 26 spills
+// book1's set (C3) on the compressed BVH4 at 5 waves too (96 VGPRs, 1 spilled with the default
+// scheduler, 13 LDS stack entries): C3 -1.2 % with the ILP scheduler's 26 spills
 // (profiles/r5_waves5_ab.jsonl), -5.5 % more without them; book2's set at 5 waves lost 3 %
 // (31 spilled), it stays at 4
 #define MESH_QWAVES 5
 #endif
 #ifndef MESH_QSHORT
-#define MESH_QSHORT 12
+#define MESH_QSHORT 13
 #endif
 #ifndef FT_TEX_WAVES
 #define FT_TEX_WAVES 4
