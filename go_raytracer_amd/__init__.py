@@ -619,25 +619,43 @@ def tune(name, value):
     check(lib().rt_tune_set(name.encode(), v))
 
 
+def tune_get(name):
+    """The text knob `name` is set to, or None when it is at its default."""
+    n = int(lib().rt_tune_get(name.encode(), None, 0))
+    check(n)
+    if n == 0:
+        return None
+    buf = C.create_string_buffer(n)
+    check(int(lib().rt_tune_get(name.encode(), buf, n)))
+    return buf.value.decode()
+
+
 def untune(name=None):
     """Clear one knob, or every knob (name None)."""
     check(lib().rt_tune_set(None if name is None else name.encode(), None))
 
 
 class tuning:
-    """Context manager: ``with rt.tuning(RT_SPLIT_MIN=0): ...`` sets knobs, then clears them."""
+    """Context manager: ``with rt.tuning(RT_SPLIT_MIN=0): ...`` sets knobs, then puts back the
+    values they had on entry (cleared if they were unset)."""
 
     def __init__(self, **knobs):
         self.knobs = knobs
+        self.saved = {}
 
     def __enter__(self):
-        for k, v in self.knobs.items():
-            tune(k, v)
+        self.saved = {k: tune_get(k) for k in self.knobs}
+        try:
+            for k, v in self.knobs.items():
+                tune(k, v)
+        except BaseException:
+            self.__exit__()
+            raise
         return self
 
     def __exit__(self, *a):
-        for k in self.knobs:
-            untune(k)
+        for k, v in self.saved.items():
+            tune(k, v)
 
 
 def tune_from_env(environ=None):

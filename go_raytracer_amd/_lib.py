@@ -137,6 +137,7 @@ SIGNATURES = {
     "rt_last_error": (C.c_char_p, []),
     "rt_abi_version": (_I, []),
     "rt_tune_set": (_I, [C.c_char_p, C.c_char_p]),
+    "rt_tune_get": (_I, [C.c_char_p, C.c_char_p, C.c_int32]),
     "rt_tune_list": (_I, [C.c_int32, C.POINTER(C.c_char_p), C.POINTER(C.c_int32)]),
     "rt_tree_create": (_I, [C.POINTER(_P)]),
     "rt_tree_destroy": (_I, [_P]),

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 enum {
   RT_OK = 0,
@@ -44,9 +44,15 @@ int rt_abi_version(void);
  * differs from its default only after the caller sets it here, and rt_scene_info.tuned /
  * rt_stats.tuned report how many knobs were set when the scene was created / the render
  * ran (the reference is configured through Camera fields only, camera.go:181-207).
- * value: a number as text (or a file path for RT_WAVE_TIMES); NULL clears the knob;
- * name NULL clears every knob.  Unknown names return RT_ERR_INVALID.  Process-wide. */
+ * value: a number as text (or a file path for RT_WAVE_TIMES, host|device|auto for
+ * RT_BVH_BUILDER); NULL clears the knob; name NULL clears every knob.  Unknown names, text
+ * that is not one whole number, and numbers outside the knob's range (e.g. RT_STEP_BUDGET
+ * below 1) return RT_ERR_INVALID and leave the knob as it was.  Process-wide. */
 int rt_tune_set(const char* name, const char* value);
+/* The value knob `name` is set to: returns 0 when it is not set, else the value's length + 1
+ * (the buffer size it needs), copying at most cap - 1 bytes and a NUL into buf when buf is not
+ * NULL and cap > 0.  Unknown names return RT_ERR_INVALID. */
+int rt_tune_get(const char* name, char* buf, int32_t cap);
 /* Knob i's name and whether it may change image bits (the others move work only); returns
  * the number of knobs (i < 0: just the count). */
 int rt_tune_list(int32_t i, const char** name, int32_t* changes_bits);

@@ -34,8 +34,9 @@ def test_bindings_cover_header(rt):
 
 def test_abi_version(rt):
     # 2: rt_render_multi, rt_stats.overflow_samples; 3: rt_tune_set (no environment reads),
-    # rt_scene_info.tuned, rt_stats.tuned / chunk_records
-    assert rt.lib().rt_abi_version() == 3
+    # rt_scene_info.tuned, rt_stats.tuned / chunk_records; 4: rt_tune_get, rt_tune_set refuses
+    # values that are not a number in the knob's range
+    assert rt.lib().rt_abi_version() == 4
 
 
 @pytest.mark.skipif(shutil.which("gcc") is None, reason="no C compiler")
@@ -143,3 +144,37 @@ def test_tuning_is_explicit_and_reported(rt, tune):
     t, cam, w, l = rt.demo_scene("book1")
     with rt.Scene(t, w, l) as sc:
         assert sc.info()["tuned"] == 0
+
+
+@pytest.mark.parametrize("name,value", [
+    ("RT_STEP_BUDGET", "0"), ("RT_STEP_BUDGET", "-3"), ("RT_STEP_BUDGET", "abc"),
+    ("RT_STEP_BUDGET", "5x"), ("RT_STEP_BUDGET", ""), ("RT_SHADE_MIN", "0"), ("RT_TAIL_K", "0"),
+    ("RT_CHUNK_NEED", "1e3"), ("RT_PARTS_LOG2", "7"), ("RT_BVH_CT", "nan"), ("RT_QBVH", "2"),
+    ("RT_BVH_BUILDER", "gpu"), ("RT_GRAB_MIN", "99999999999999999999"),
+])
+def test_tune_set_refuses_bad_values(rt, tune, name, value):
+    """a scheduling knob out of range (a step budget of 0 would leave every traversal
+    without steps and the fused loop spinning) is refused with RT_ERR_INVALID, before any render,
+    and the knob keeps its previous value."""
+    tune(name, {"RT_BVH_BUILDER": "host", "RT_BVH_CT": "2.5"}.get(name, "1"))
+    before = rt.tune_get(name)
+    with pytest.raises(rt.RtError, match="rt_tune_set"):
+        rt.tune(name, value)
+    assert rt.tune_get(name) == before
+
+
+def test_tune_get_and_tuning_restores(rt, tune):
+    """rt_tune_get reads a knob back; rt.tuning puts back the values knobs had on entry."""
+    assert rt.tune_get("RT_GRAB_MIN") is None
+    with pytest.raises(rt.RtError):
+        rt.tune_get("RT_NOT_A_KNOB")
+    tune("RT_GRAB_MIN", 64)
+    assert rt.tune_get("RT_GRAB_MIN") == "64"
+    assert int(rt.lib().rt_tune_get(b"RT_GRAB_MIN", None, 0)) == 3
+    with rt.tuning(RT_GRAB_MIN=8, RT_SPLIT_MIN=0):
+        assert rt.tune_get("RT_GRAB_MIN") == "8" and rt.tune_get("RT_SPLIT_MIN") == "0"
+    assert rt.tune_get("RT_GRAB_MIN") == "64" and rt.tune_get("RT_SPLIT_MIN") is None
+    with pytest.raises(rt.RtError):
+        with rt.tuning(RT_SPLIT_MIN=1, RT_STEP_BUDGET=0):
+            pass
+    assert rt.tune_get("RT_SPLIT_MIN") is None and rt.tune_get("RT_STEP_BUDGET") is None

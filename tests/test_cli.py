@@ -89,3 +89,21 @@ def test_cli_image_matches_harness(rt, gpu, tmp_path, scene, name):
     js = json.loads(prof.read_text())
     assert js["scene"] == name and js["samples"] == st["samples"] == 40 * img.shape[0] * 9
     assert np.isfinite(js["samples_per_s"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene,slices", [(1, 1024), (1, 7), (4, 1024), (6, 1024)])
+def test_cli_short_progress_slices_terminate(rt, gpu, tmp_path, scene, slices):
+    """the r5i session's book1 render at 40 px, 9 spp with progress slices
+    never finished its last slice (the build then carried an in-shading chunk pool, removed in
+    8001c64).  Slices shorter than one chunk batch (3,120 chunks over 1,024 launches), with the
+    drain split on, in a child process with a time limit: every launch must end.  The image
+    is the one of a single launch (exact pixel sums)."""
+    out1, out2 = tmp_path / "a.ppm", tmp_path / "b.ppm"
+    common = ["-S", str(scene), "-width", "40", "-spp", "9", "-depth", "6", "-seed", "5"]
+    r = run(*common, "-o", str(out1), "-slices", str(slices), "-progress", timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert "100.0%" in r.stderr
+    r = run(*common, "-o", str(out2), timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert out1.read_bytes() == out2.read_bytes()
