@@ -1234,8 +1234,10 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   const bool long_shade = ft_set == FT_ALL || (ft_set & FT_NOISE);
   // (book2 at full size: 7 steps and 40 ready lanes -0.7 % against 8 / 32,
   // profiles/r5_c4_c5_knobs_full.jsonl)
-  p.step_budget = env_int("RT_STEP_BUDGET", f_lds ? (1 << 30) : big_tree ? (long_shade ? 7 : 5) : 10);
-  p.shade_min = (uint32_t)env_int("RT_SHADE_MIN", f_lds ? 1 : long_shade ? 40 : big_tree ? 32 : 1);
+  // (clamped where read, as every scheduling knob: a round without a traversal step would
+  // never finish a traversal)
+  p.step_budget = std::max(1, env_int("RT_STEP_BUDGET", f_lds ? (1 << 30) : big_tree ? (long_shade ? 7 : 5) : 10));
+  p.shade_min = (uint32_t)std::max(1, env_int("RT_SHADE_MIN", f_lds ? 1 : long_shade ? 40 : big_tree ? 32 : 1));
   // chunks per refill of a wave's batch (one returning atomic on the chunk
   // counter each): C2 grab sweep (profiles/r1_grab_sweep.jsonl) 64 -> 128:
   // -4 % at 1-2 ranks' shares; 256 for small chunks: -11 % on the 8-GPU share
