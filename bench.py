@@ -208,15 +208,17 @@ def roofline(db, key, kernel, ms, seg, smp, pix, full_smp):
         a = valu / ms / 1e6
         r.update(achieved=round(a, 2), frac=round(a / PEAK_VALU_GIPS, 4),
                  valu_insts_per_launch=valu)
-        # SIMD cycles available per VALU wave-instruction of this launch.  `peak` assumes 2
-        # cycles for every instruction; measured on gfx950 (tools/instr_rate.hip,
-        # profiles/r4_instr_rate.jsonl, 8 waves per SIMD) fp32 add/mul/fma, 32-bit integer
-        # add, logic, shifts and moves take ~2.4, min/max, compares, conversions, 32-bit
-        # multiplies, packed fp32 and fp64 ~4.2, v_readlane 6.3, rcp/sqrt 8.2.  Weighted by
-        # the kernels' static instruction mix that is ~3.4 cycles (C2's and C4's kernels at
-        # HEAD, round 4), so a figure near 3.4 means the SIMDs issue back to back
+        # SIMD cycles available per VALU wave-instruction of this launch (`peak` assumes 2)
         r["simd_cycles_per_valu"] = round(4 * 256 * 2.4e6 * ms / valu, 3)
-        r["issue_cost_source"] = "profiles/r4_instr_rate.jsonl"
+    if pmc.get("valu_busy_counter"):
+        # counter-measured VALU busy of the SIMDs (tools/pmc_traffic.py): SQ_ACTIVE_INST_VALU
+        # quad-cycles x 4 / 2 cycles per wave64 instruction at the SIMD-32 pipe, over the
+        # SIMD cycles of the same launch (1,024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs).  It charges
+        # long instructions (transcendentals, fp64) their real occupancy, so 1 - valu_busy
+        # is the measured headroom of the VALU pipe; the 2-cycle `frac` prices every
+        # instruction alike
+        r["valu_busy"] = {"frac": round(pmc["valu_busy_counter"], 4),
+                          "source": "SQ_ACTIVE_INST_VALU*4/2 / (1024*GRBM_GUI_ACTIVE/8)"}
     if hbm:
         g = hbm / ms / 1e6
         r["hbm_counter"] = {"achieved": round(g, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",

@@ -69,6 +69,18 @@ RT_D void finish_hit(const Params& P, const Path& s, Hit& best) {
 // spilled 32 VGPRs in the traversal loop and lost 24 %
 #define TRI_QWAVES 5
 #endif
+// RT_QTOP=N (experiment): the compressed BVH4's first N items (BFS order: the root and its
+// top levels, which nearly every ray visits) staged in dynamic LDS at kernel start and read
+// from there, off the vector-memory return path that bounds C5; one LDS stack entry fewer
+// so five blocks still fit
+#ifdef RT_QTOP
+#ifndef TRI_QSHORT
+#define TRI_QSHORT 12
+#endif
+#ifndef MESH_QSHORT
+#define MESH_QSHORT 12
+#endif
+#endif
 #ifndef TRI_QSHORT
 // 13 LDS traversal-stack entries fill five blocks' LDS (5 x 31,776 B of 160 KiB): C5 -1.5 %,
 // C3 -0.3 % against 12, 10 +4.5 % (profiles/r5_qshort_ab.jsonl)
@@ -173,6 +185,12 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
   if constexpr (HAS(FT_NOISE)) stage_perlin(P.sc);  // before stage_nodes' barrier
   if constexpr (cam_mode(FT) == 1) stage_camera(P);
   const bool recs_lds = LDS && TREE != 8 && stage_nodes(P, lnodes, TREE == 4 ? 8 : 4);
+#ifdef RT_QTOP
+  if constexpr (TREE == 5) {  // the top items into the dynamic LDS (sized at launch)
+    const uint32_t nq = 4u * (uint32_t)min(RT_QTOP, P.sc.n_nodes);
+    for (uint32_t i = threadIdx.x; i < nq; i += blockDim.x) st_lds(&lnodes[i], ld_glb(P.sc.nodes + i));
+  }
+#endif
   if (!LDS) __syncthreads();  // staged tables visible to every wave (stage_nodes ends with one)
   const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;  // weight-stack column
   const TravStack ts = {&lstack[threadIdx.x], P.ostack + slot, P.stack_cols, fused_short(FT, TREE)
@@ -274,6 +292,7 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
         // TREE 5: the compressed BVH4 (64-B items, host_qbvh.cpp), read through L1/L2
         const int nsteps = trav_steps<LDS, FT, TREE == 4 || TREE == 5, TREE == 5>(
             P.sc, lnodes, recs_lds, ts, s.o, s.d, s.time, 0.001f, tr, P.step_budget);
+        retest_near<FT>(P.sc, s.o, s.d, 0.001f, tr);
 #ifdef RT_PHASES
         ph_steps(nsteps);
 #endif

@@ -130,6 +130,12 @@ struct Scene {
   int multi_dev = -1;
   void* rccl = nullptr;                             // RCCL gather state (rt_render.hip RcclGather)
   Progress prog;
+  // the compressed BVH4 (host_qbvh.cpp), built on the host once, at the first render that
+  // can traverse it (rt_render.hip ensure_qbvh), then uploaded per device
+  std::mutex qb_mu;
+  bool qb_built = false;
+  std::vector<F4> qb;
+  size_t qb_items = 0;
 };
 
 // host_flatten.cpp

@@ -36,7 +36,9 @@ RT_D f3 cross(f3 a, f3 b) {
 RT_D float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 RT_D float length(f3 a) { return fsqrt(dot(a, a)); }
 RT_D float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
-RT_D f3 unit(f3 a) { return a * rcp(length(a)); }  // UnitVector vec.go:125
+// UnitVector vec.go:125 as one v_rsq_f32 (1 ulp) instead of v_sqrt + v_rcp (two roundings,
+// two transcendental issues at a quarter of the VALU rate)
+RT_D f3 unit(f3 a) { return a * __builtin_amdgcn_rsqf(dot(a, a)); }
 RT_D bool finite3(f3 a) { return isfinite(a.x) && isfinite(a.y) && isfinite(a.z); }
 
 RT_D uint32_t fbits(float f) { return __float_as_uint(f); }
@@ -78,6 +80,17 @@ RT_D Onb make_onb(f3 n) {
   o.v = unit(cross(n, a));
   // unit(cross(n, v)) = cross(n, v) / |n| = cross(w, v): w and v are unit and orthogonal, so
   // the reference's third normalisation (onb.go:23) is the identity up to rounding
+  o.u = cross(o.w, o.v);
+  return o;
+}
+// NewONB of a normal that is already unit (every shading normal: quad and triangle normals are
+// stored normalised, sphere normals divided by their length): w = n, whose normalisation the
+// reference repeats (onb.go:21) and which changes it by at most an ulp here
+RT_D Onb make_onb_unit(f3 n) {
+  Onb o;
+  o.w = n;
+  f3 a = fabsf(n.x) > 0.9f ? mk3(0, 1, 0) : mk3(1, 0, 0);
+  o.v = unit(cross(n, a));
   o.u = cross(o.w, o.v);
   return o;
 }
@@ -429,7 +442,7 @@ RT_D uint32_t unit_ab_rej(float a, float b) {
 }
 // Triangle.Hit objects.go:408-461 (hit_tri_rec's arithmetic)
 RT_D uint32_t hit_tri_rec_m(const F4 r[4], f3 o, f3 d, float tmin, float tmax, float& t_out,
-                            float& u_out, float& v_out) {
+                            float& u_out, float& v_out, bool& near) {
   const f3 e0 = xyz(r[1]), e1 = xyz(r[2]);
   const f3 pvec = cross(d, e1);
   const float det = dot(e0, pvec);
@@ -444,8 +457,62 @@ RT_D uint32_t hit_tri_rec_m(const F4 r[4], f3 o, f3 d, float tmin, float tmax, f
   v_out = v;
   // |det| >= 1e-8, 0 <= u <= 1, v >= 0, u + v <= 1, tmin <= t <= tmax
   const uint32_t a = sign_any3(fabsf(det) - 1e-8f, u, 1.0f - u);
-  const uint32_t b = sign_any3(v, 1.0f - (u + v), t - tmin);
-  return spread_sign(__builtin_amdgcn_bitop3_b32(a, b, fbits(tmax - t), 0xFE));
+  const float w = 1.0f - (u + v);
+  const uint32_t b = sign_any3(v, w, t - tmin);
+  uint32_t rej = spread_sign(__builtin_amdgcn_bitop3_b32(a, b, fbits(tmax - t), 0xFE));
+#ifdef RT_TRI_EDGE64  // opt-in build (DESIGN.md §7 "Triangle edges"): +5.6 % C5 time, parity unchanged
+  // Near-edge rejections.  In fp32, u, v and w carry an absolute error of
+  // a few eps * |o - v0| * |d| * |e| / |det| (the triple products cancel: ~1e-4 for camera rays
+  // 14 units from the 1M-triangle mesh's 0.01-unit triangles; tools/tri_edge_error.py measures
+  // at most 6.2 times that bound).  Two triangles sharing an edge compute their edge functions
+  // from different vertices, so their errors differ, and a ray within that error of the edge
+  // can be rejected by both: a hole, through which the GPU saw the mesh behind where the fp64
+  // oracle hit it (C5's vertex-0 forks: u = 2e-4 against an fp32 error of ~2e-4).  A test
+  // rejected only by a barycentric that is within 8 times the bound below 0 is flagged
+  // `near`; the traversal keeps it (trav_steps `pend`) and tri_hit64 repeats Triangle.Hit in
+  // fp64 on the same fp32 ray and vertices after the round (retest_near).  Below the band the
+  // fp64 test rejects too, so every triangle the fp64 test accepts is accepted: no hole.
+  // (fp32 acceptances just inside an edge stay: they cover the surface twice, never open it.)
+  const float amax = fmaxf(fmaxf(fabsf(e0.x), fabsf(e0.y)), fmaxf(fabsf(e0.z), fabsf(e1.x)));
+  const float emax = fmaxf(amax, fmaxf(fabsf(e1.y), fabsf(e1.z)));
+  const float tmax3 = fmaxf(fmaxf(fabsf(tvec.x), fabsf(tvec.y)), fabsf(tvec.z));
+  const float dmax3 = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
+  const float bnd = 0x1p-21f * tmax3 * dmax3 * emax * fabsf(inv);
+  const float bmin = fminf(fminf(u, v), w);
+  // rejected with det and t in range (signs clear): by a barycentric, the smallest in the band
+  const uint32_t other = sign_any3(fabsf(det) - 1e-8f, t - tmin, tmax - t);
+  near = rej != 0u && (int32_t)other >= 0 && bmin + bnd >= 0.0f;
+#else
+  near = false;
+#endif
+  return rej;
+}
+// Triangle.Hit (objects.go:408-461) in fp64 on the fp32 ray and the triangle's fp32 vertex
+// data (sc.tri: the same v0, e0, e1 as its leaf record), closed interval [tmin, tmax]: the
+// re-test of a near-edge rejection (hit_tri_rec_m `near`)
+RT_D bool tri_hit64(const DevScene& sc, uint32_t idx, f3 o, f3 d, float tmin, float tmax,
+                    float& t_out, float& u_out, float& v_out) {
+  const F4* tr = sc.tri + 3 * (size_t)idx;
+  const F4 V0 = tr[0], E0 = tr[1], E1 = tr[2];
+  const double ax = E0.x, ay = E0.y, az = E0.z, bx = E1.x, by = E1.y, bz = E1.z;
+  const double dx = d.x, dy = d.y, dz = d.z;
+  const double px = dy * bz - dz * by, py = dz * bx - dx * bz, pz = dx * by - dy * bx;
+  const double det = ax * px + ay * py + az * pz;
+  if (!(fabs(det) >= 1e-8)) return false;
+  double inv = __builtin_amdgcn_rcp(det);  // + one Newton step (refine_tri_hit's)
+  inv = fma(inv, fma(-det, inv, 1.0), inv);
+  const double tx = (double)o.x - V0.x, ty = (double)o.y - V0.y, tz = (double)o.z - V0.z;
+  const double u = (tx * px + ty * py + tz * pz) * inv;
+  if (u < 0.0 || u > 1.0) return false;
+  const double qx = ty * az - tz * ay, qy = tz * ax - tx * az, qz = tx * ay - ty * ax;
+  const double v = (dx * qx + dy * qy + dz * qz) * inv;
+  if (v < 0.0 || u + v > 1.0) return false;
+  const double t = (bx * qx + by * qy + bz * qz) * inv;
+  if (t < (double)tmin || t > (double)tmax) return false;
+  t_out = (float)t;
+  u_out = (float)u;
+  v_out = (float)v;
+  return true;
 }
 // quad.Hit objects.go:167-196 (hit_quad_rec's arithmetic)
 RT_D uint32_t hit_quad_rec_m(const F4 r[4], f3 o, f3 d, float tmin, float tmax, float& t_out,
@@ -486,7 +553,8 @@ RT_D bool hit_record(const F4 r[4], f3 o, f3 d, float iy, float time, float tmin
 // hit_record as a reject mask (the traversal's closest-hit update is then v_bitop3 selects)
 template <uint32_t FT>
 RT_D uint32_t hit_record_m(const F4 r[4], f3 o, f3 d, float iy, float time, float tmin, float tmax,
-                           float& t, float& u, float& v, uint32_t& ref) {
+                           float& t, float& u, float& v, uint32_t& ref, bool& near) {
+  near = false;
   ref = fbits(r[0].w);
   const uint32_t type = ref >> 30;
   if (HAS(FT_BOX) && type == PRIM_BOX) {
@@ -495,7 +563,7 @@ RT_D uint32_t hit_record_m(const F4 r[4], f3 o, f3 d, float iy, float time, floa
     return hit_box_rec(r, o, d, iy, tmin, tmax, t, ref) ? 0u : ~0u;
   }
   if (!HAS(FT_SPHERE | FT_TRI) || type == PRIM_QUAD) return hit_quad_rec_m(r, o, d, tmin, tmax, t, u, v);
-  if (HAS(FT_TRI) && (!HAS(FT_SPHERE) || type == PRIM_TRI)) return hit_tri_rec_m(r, o, d, tmin, tmax, t, u, v);
+  if (HAS(FT_TRI) && (!HAS(FT_SPHERE) || type == PRIM_TRI)) return hit_tri_rec_m(r, o, d, tmin, tmax, t, u, v, near);
   u = v = 0.0f;
   return hit_sphere_rec(r, o, d, time, tmin, tmax, t) ? 0u : ~0u;
 }

@@ -159,7 +159,10 @@ RT_D uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn
 // shares, not the absolute cycles.
 enum { PH_GRAB, PH_TRAV, PH_MEDIA, PH_SHADE, PH_TEX, PH_LIGHT, PH_TERM, PH_LOOP,
        PH_TRAV_LANES, PH_TRAV_ROUNDS, PH_SHADE_LANES, PH_SHADE_ROUNDS, PH_STEP_LANES,
-       PH_STEP_WAVE, PH_QNODE_LANES, PH_QLEAF_LANES, PH_QMIXED, PH_QITERS, PH_N = 18 };
+       PH_STEP_WAVE, PH_QNODE_LANES, PH_QLEAF_LANES, PH_QMIXED, PH_QITERS,
+       // compressed-BVH steps: lanes on the first active lane's item, distinct items per
+       // iteration, and lanes on items of BFS levels 0-3 (item < 85) / 4-5 (item < 1365)
+       PH_QSAME, PH_QUNIQ, PH_QTOP, PH_QMID, PH_N = 22 };
 constexpr int kWaveRec = 4 + PH_N;  // {start, end, segments, pad, phases...} per wave
 #ifdef RT_PHASES
 __shared__ unsigned long long g_ph[4][PH_N];
@@ -433,7 +436,22 @@ struct Trav {
                  // from LDS in the background (the refill lands while the popped
                  // subtree is traversed), taking the LDS latency off the pop
   Hit best;
+  // a triangle the last round's fp32 test rejected within its rounding error of an edge
+  // (hit_tri_rec_m `near`), for tri_hit64 after trav_steps; PRIM_NONE: none.  Set only by the
+  // round that ends on it, consumed before the next one (retest_near)
+  uint32_t pend;
 };
+// the fp64 re-test of a round's near-edge rejection (hit_tri_rec_m): taken when it hits
+// within the closest hit so far, as the fp32 test would have taken it.  Divergent and rare.
+template <uint32_t FT>
+RT_D void retest_near(const DevScene& sc, f3 o, f3 d, float tmin, Trav& tr) {
+  if constexpr (HAS(FT_TRI)) {
+    if (tr.pend != PRIM_NONE) {
+      float t, u, v;
+      if (tri_hit64(sc, tr.pend & 0x3FFFFFFFu, o, d, tmin, tr.best.t, t, u, v)) tr.best = {t, u, v, tr.pend};
+    }
+  }
+}
 // A new ray: the traversal state, and the spheres kept out of the BVH (radius >=
 // kBigSphereR: the ground spheres of book1 and the mesh scene) tested first, in fp64, by
 // every lane at once (a uniform loop over scalar-loaded records), so the BVH's sphere
@@ -533,6 +551,9 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
     }
   };
   const f3 inv = tr.inv;
+  // a near-edge rejection of this round, re-tested in fp64 after it (retest_near); a second
+  // one ends the round before its step, which the next round repeats
+  uint32_t pend = PRIM_NONE;
   int n = 0;
   for (; n < budget && cur != TRAV_DONE; ++n) {
     if constexpr (QN) {
@@ -545,14 +566,36 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
         PH_CNT(PH_QNODE_LANES, __popcll(mn));
         PH_CNT(PH_QMIXED, (ml && mn) ? 1 : 0);
         PH_CNT(PH_QITERS, 1);
+        const uint32_t item = cur & 0x0FFFFFFFu;
+        const uint32_t first_item = __builtin_amdgcn_readfirstlane(item);
+        PH_CNT(PH_QSAME, __popcll(__ballot(item == first_item)));
+        PH_CNT(PH_QTOP, __popcll(__ballot(item < 85u)));
+        PH_CNT(PH_QMID, __popcll(__ballot(item >= 85u && item < 1365u)));
+        unsigned long long left = __ballot(1);
+        uint32_t uniq = 0;
+        while (left) {  // distinct items among the active lanes (debug build only)
+          const uint32_t lead = (uint32_t)(__ffsll((long long)left) - 1);
+          const uint32_t vi = __builtin_amdgcn_readlane(item, lead);
+          left &= ~__ballot(item == vi);
+          ++uniq;
+        }
+        PH_CNT(PH_QUNIQ, uniq);
       }
 #endif
       const F4* it = (const F4*)((const char*)sc.nodes + ((cur & 0x0FFFFFFFu) << 6));
       F4 v[4];
       // (all four unconditionally: a leaf lane skipping the fourth when the scene has no
       // quads made hipcc wait for the first loads before the predicated one, C5 +1.9 %)
+#ifdef RT_QTOP
+      if ((cur & 0x0FFFFFFFu) < (uint32_t)RT_QTOP) {  // a top item: its LDS copy (k_fused)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = ld_glb(it + e);
+        for (int e = 0; e < 4; ++e) v[e] = ld_lds(lnodes + 4 * (cur & 0x0FFFFFFFu) + e);
+      } else
+#endif
+      {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = ld_glb(it + e);
+      }
       if (!leaf) {
         float tn[4];
         uint32_t ch[4];
@@ -577,11 +620,19 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
       } else {
         float t, u, vv;
         uint32_t ref;
-        const uint32_t rej = hit_record_m<FT>(v, o, d, inv.y, time, tmin, tr.best.t, t, u, vv, ref);
+        bool near;
+        const uint32_t rej = hit_record_m<FT>(v, o, d, inv.y, time, tmin, tr.best.t, t, u, vv, ref, near);
         tr.best.t = bitsf(pick_by(fbits(t), fbits(tr.best.t), rej));
         tr.best.u = bitsf(pick_by(fbits(u), fbits(tr.best.u), rej));
         tr.best.v = bitsf(pick_by(fbits(vv), fbits(tr.best.v), rej));
         tr.best.ref = pick_by(ref, tr.best.ref, rej);
+        if (HAS(FT_TRI) && near) {
+          if (pend != PRIM_NONE) {  // (rejected: nothing changed) this leaf again next round
+            n = budget;
+            continue;
+          }
+          pend = ref;
+        }
       }
       if (sp == 0) cur = TRAV_DONE;
       else cur = stack.pop(--sp);
@@ -687,17 +738,31 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
       } else {
         const uint32_t count = (cur & 15u) + 1u;
         F4 rec[4] = {v[0], v[1], v[2], v[3]};
-        for (uint32_t k = 0;;) {
+        uint32_t k = 0;
+        for (;;) {
           float t, u, vv;
           uint32_t ref;
-          const uint32_t rej = hit_record_m<FT>(rec, o, d, inv.y, time, tmin, tr.best.t, t, u, vv, ref);
+          bool near;
+          const uint32_t rej = hit_record_m<FT>(rec, o, d, inv.y, time, tmin, tr.best.t, t, u, vv, ref, near);
           tr.best.t = bitsf(pick_by(fbits(t), fbits(tr.best.t), rej));
           tr.best.u = bitsf(pick_by(fbits(u), fbits(tr.best.u), rej));
           tr.best.v = bitsf(pick_by(fbits(vv), fbits(tr.best.v), rej));
           tr.best.ref = pick_by(ref, tr.best.ref, rej);
-          if (++k >= count) break;
+          if (HAS(FT_TRI) && near) {
+            if (pend != PRIM_NONE) {  // the round ends before this prim (repeated next round)
+              n = budget;
+              break;
+            }
+            pend = ref;
+          }
+          ++k;
+          if (k >= count) break;
           const F4* q = sc.leafprims + 4 * (size_t)(first + k);
           for (int e = 0; e < 4; ++e) rec[e] = ld_glb(q + e);
+        }
+        if (HAS(FT_TRI) && k < count) {
+          cur = LEAF_BIT | ((first + k) << 4) | (count - k - 1u);
+          continue;
         }
       }
       if (sp == 0) cur = TRAV_DONE;
@@ -772,7 +837,8 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
     } else {
       uint32_t first = (cur >> 4) & 0x7FFFFFFu, count = (cur & 15u) + 1u;
       // leaf records are contiguous: no ref indirection, all four loads issue at once
-      for (uint32_t k = 0; k < count; ++k) {
+      uint32_t k = 0;
+      for (; k < count;) {
         const uint32_t ri = 4 * (first + k);
         F4 rec[4];
         if (LDS && recs_lds) {
@@ -785,11 +851,24 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
         }
         float t, u, v;
         uint32_t ref;
-        const uint32_t rej = hit_record_m<FT>(rec, o, d, inv.y, time, tmin, tr.best.t, t, u, v, ref);
+        bool near;
+        const uint32_t rej = hit_record_m<FT>(rec, o, d, inv.y, time, tmin, tr.best.t, t, u, v, ref, near);
         tr.best.t = bitsf(pick_by(fbits(t), fbits(tr.best.t), rej));
         tr.best.u = bitsf(pick_by(fbits(u), fbits(tr.best.u), rej));
         tr.best.v = bitsf(pick_by(fbits(v), fbits(tr.best.v), rej));
         tr.best.ref = pick_by(ref, tr.best.ref, rej);
+        if (HAS(FT_TRI) && near) {
+          if (pend != PRIM_NONE) {  // the round ends before this prim (repeated next round)
+            n = budget;
+            break;
+          }
+          pend = ref;
+        }
+        ++k;
+      }
+      if (HAS(FT_TRI) && k < count) {  // the leaf's other prims first, next round
+        cur = LEAF_BIT | ((first + k) << 4) | (count - k - 1u);
+        continue;
       }
     }
     if (sp == 0) {
@@ -804,6 +883,7 @@ RT_D int trav_steps(const DevScene& sc, const F4* lnodes, bool recs_lds, const T
   tr.cur = cur;
   tr.sp = sp;
   tr.top = top;
+  tr.pend = pend;
   return n;
 }
 
@@ -908,11 +988,15 @@ RT_D int trav_steps8(const DevScene& sc, const TravStack& stack, f3 o, f3 d, flo
       for (uint32_t k = 0;;) {
         float t, u, vv;
         uint32_t ref;
-        const uint32_t rej = hit_record_m<FT>(rec, o, d, inv.y, time, tmin, tr.best.t, t, u, vv, ref);
+        bool near;
+        const uint32_t rej = hit_record_m<FT>(rec, o, d, inv.y, time, tmin, tr.best.t, t, u, vv, ref, near);
         tr.best.t = bitsf(pick_by(fbits(t), fbits(tr.best.t), rej));
         tr.best.u = bitsf(pick_by(fbits(u), fbits(tr.best.u), rej));
         tr.best.v = bitsf(pick_by(fbits(vv), fbits(tr.best.v), rej));
         tr.best.ref = pick_by(ref, tr.best.ref, rej);
+        // (opt-in BVH8 kernels: the near-edge fp64 re-test applied at once, not deferred)
+        if (HAS(FT_TRI) && near && tri_hit64(sc, ref & 0x3FFFFFFFu, o, d, tmin, tr.best.t, t, u, vv))
+          tr.best = {t, u, vv, ref};
         if (++k >= count) break;
         const F4* q = sc.recs8 + 4 * (size_t)(first + k);
         for (int e = 0; e < 4; ++e) rec[e] = ld_glb(q + e);
@@ -1254,7 +1338,10 @@ RT_D void trace_world(const DevScene& sc, const F4* lnodes, bool recs_lds, const
                       f3 o, f3 d, float time, float tmin, Hit& best) {
   Trav tr;
   trav_init<FT>(sc, o, d, time, tr);
-  trav_steps<LDS, FT>(sc, lnodes, recs_lds, stack, o, d, time, tmin, tr, 0x7FFFFFFF);
+  do {  // a near-edge rejection ends a round early (retest_near)
+    trav_steps<LDS, FT>(sc, lnodes, recs_lds, stack, o, d, time, tmin, tr, 0x7FFFFFFF);
+    retest_near<FT>(sc, o, d, tmin, tr);
+  } while (tr.cur != TRAV_DONE);
   best = tr.best;
 }
 
@@ -2112,7 +2199,7 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
         PH_ADD(PH_TEX, t_tex);
         PH_T(t_light);
         Onb b;
-        if (!iso) b = make_onb(n);
+        if (!iso) b = make_onb_unit(n);
         if (rt_unit_f(r.v[0]) < 0.5f) {
           ndir = lights_random<FT>(sc, p, r);
         } else if (iso) {

@@ -203,6 +203,9 @@ struct DeviceScene {
   uint32_t root2 = PRIM_NONE;
   int32_t n_nodes2 = 0;
   const F4* qnodes = nullptr;       // compressed BVH4 (host_qbvh.cpp): 64-B items, root item 0
+  size_t qitems = 0;
+  std::mutex qmu;                   // ensure_qbvh: the first render that needs it uploads it
+  bool q_done = false;
   ~DeviceScene() {
     for (void* p : allocs) (void)hipFree(p);
   }
@@ -471,13 +474,7 @@ static int upload_scene(const Scene* s, DeviceScene* ds) {
     d.nodes = base;
     d.leafprims = base ? base + rec0 : nullptr;
   }
-  {  // the compressed BVH4 of trees read through L1/L2 (single-prim leaves, render_impl: tree 5)
-    std::vector<F4> qb;
-    size_t items = 0;
-    if ((rc = build_qbvh(h, recs, &qb, &items)) != RT_OK)
-      return rc;
-    if (items && (rc = upload(ds, qb, &ds->qnodes)) != RT_OK) return rc;
-  }
+  // (the compressed BVH4 is built and uploaded on demand: ensure_qbvh)
   // the BVH2 and the record-loop pairs serve tiny scenes only (render_impl's tree
   // choice: <= 64 leaf entries); a 1M-triangle scene would upload 64 MB of BVH2
   const size_t tiny = (size_t)std::max(64, env_int("RT_BRUTE_MAX", kBruteMax));
@@ -918,6 +915,32 @@ struct Gather {
   int dst_device;
 };
 
+// The compressed BVH4 of a tree read through L1/L2 (render_impl's tree 5), on `device`
+// (current): built on the host once per scene and uploaded once per device, by the first
+// render whose kernel can traverse it -- not for LDS-resident trees, record-loop scenes or
+// RT_QBVH=0 renders (~85 MB of HBM per GPU for the 1M-triangle mesh otherwise).
+static int ensure_qbvh(Scene* s, DeviceScene* ds) {
+  std::lock_guard<std::mutex> lk(ds->qmu);
+  if (ds->q_done) return RT_OK;
+  {
+    std::lock_guard<std::mutex> hk(s->qb_mu);
+    if (!s->qb_built) {
+      std::vector<F4> recs;
+      build_leaf_records(s->h, recs);
+      int rc = build_qbvh(s->h, recs, &s->qb, &s->qb_items);
+      if (rc != RT_OK) return rc;
+      s->qb_built = true;
+    }
+  }
+  if (s->qb_items) {
+    const int rc = upload(ds, s->qb, &ds->qnodes);
+    if (rc != RT_OK) return rc;
+    ds->qitems = s->qb_items;
+  }
+  ds->q_done = true;
+  return RT_OK;
+}
+
 static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_opts* opts,
                        float* out_host, float* out_dev, rt_stats* stats, int slot_id = 0,
                        const Gather* gather = nullptr) {
@@ -1018,12 +1041,19 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   // Trees read through L1/L2 with single-prim leaves take the compressed BVH4 (64-B nodes,
   // host_qbvh.cpp): the same closest hits, half the bytes per node step.  RT_QBVH=0: the
   // 128-B nodes (A/B)
-  if (mode == RT_MODE_FUSED && tree == 4 && !f_lds && ds->qnodes && env_int("RT_QBVH", 1) != 0 &&
-      pick_fused(false, ft_set, 5))
-    tree = 5;
+  if (mode == RT_MODE_FUSED && tree == 4 && !f_lds && env_int("RT_QBVH", 1) != 0 &&
+      pick_fused(false, ft_set, 5)) {
+    if ((rc = ensure_qbvh(s, ds))) return rc;
+    if (ds->qnodes) tree = 5;
+  }
   const void* fused_kernel = pick_fused(f_lds, ft_set, tree);
   if (!fused_kernel) return set_error(RT_ERR_UNSUPPORTED, "internal: no fused kernel for this scene");
+#ifdef RT_QTOP
+  const size_t fused_lds = f_lds ? 64 * (node_slots * n_nodes + (f_recs ? rec_slots : 0))
+                           : tree == 5 ? 64 * std::min<size_t>(RT_QTOP, ds->qitems) : 0;
+#else
   const size_t fused_lds = f_lds ? 64 * (node_slots * n_nodes + (f_recs ? rec_slots : 0)) : 0;
+#endif
   if (mode == RT_MODE_FUSED) {
     if ((rc = occupancy_blocks(fused_kernel, o.device, &fused_blocks, fused_lds))) return rc;
     if (o.path_slots > 0) fused_blocks = std::max(1, std::min(fused_blocks, (o.path_slots + 255) / 256));
@@ -1165,6 +1195,7 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   } else if (tree == 5) {
     p.sc.nodes = ds->qnodes;
     p.sc.root = 0;  // item 0: the root node (trav_init)
+    p.sc.n_nodes = (int32_t)std::min<size_t>(ds->qitems, 0x7FFFFFFF);  // 64-B items
   } else if (tree == 8) {
     p.sc.root = 0;  // BVH8 node 0 (trav_init)
   } else if (tree == 0) {

@@ -9,7 +9,23 @@
 #include <stdio.h>
 #include <stdint.h>
 
-#define ITERS 4096
+#define ITERS 4096  // x 8 independent chains per iteration, 8 x unrolled (below)
+
+// In-kernel timing of wave 0 of block 0: s_memtime counts shader cycles
+// (MI355X_MICROARCH.md constants table), s_memrealtime a constant 100 MHz.  The SIMD's issue
+// cost is the wave's elapsed shader cycles over the instructions issued by the waves sharing
+// its SIMD (every wave runs the same stream, all resident at once), so neither the clock
+// frequency nor the launch overhead enters it; the clock itself is reported beside it.
+__device__ unsigned long long g_tim[2];
+#define T_BEGIN                                                                           \
+  const unsigned long long _c0 = __builtin_amdgcn_s_memtime(),                            \
+                           _r0 = __builtin_amdgcn_s_memrealtime();                \
+  _Pragma("unroll 8")
+#define T_END                                                                             \
+  if (blockIdx.x == 0 && threadIdx.x == 0) {                                              \
+    g_tim[0] = __builtin_amdgcn_s_memtime() - _c0;                                        \
+    g_tim[1] = __builtin_amdgcn_s_memrealtime() - _r0;                                    \
+  }
 
 #define BODY8(OP) OP(0) OP(1) OP(2) OP(3) OP(4) OP(5) OP(6) OP(7)
 
@@ -17,11 +33,11 @@ __global__ void k_mad_u64(uint32_t* out, uint32_t seed) {
   uint64_t a[8];
   uint32_t m = 0xD2511F53u ^ seed;
   for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
-  for (int it = 0; it < ITERS; ++it) {
+  T_BEGIN for (int it = 0; it < ITERS; ++it) {
 #define OP(i) { uint64_t cc; asm volatile("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(a[i]), "=s"(cc) : "v"((uint32_t)a[i]), "s"(m)); }
     BODY8(OP)
 #undef OP
-  }
+  } T_END
   uint32_t s = 0;
   for (int i = 0; i < 8; ++i) s ^= (uint32_t)a[i] ^ (uint32_t)(a[i] >> 32);
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
@@ -30,11 +46,11 @@ __global__ void k_mul_hi(uint32_t* out, uint32_t seed) {
   uint32_t a[8];
   uint32_t m = 0xD2511F53u ^ seed;
   for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
-  for (int it = 0; it < ITERS; ++it) {
+  T_BEGIN for (int it = 0; it < ITERS; ++it) {
 #define OP(i) asm volatile("v_mul_hi_u32 %0, %1, %2" : "=v"(a[i]) : "v"(a[i]), "s"(m));
     BODY8(OP)
 #undef OP
-  }
+  } T_END
   uint32_t s = 0;
   for (int i = 0; i < 8; ++i) s ^= a[i];
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
@@ -43,11 +59,11 @@ __global__ void k_mul_lo(uint32_t* out, uint32_t seed) {
   uint32_t a[8];
   uint32_t m = 0xD2511F53u ^ seed;
   for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
-  for (int it = 0; it < ITERS; ++it) {
+  T_BEGIN for (int it = 0; it < ITERS; ++it) {
 #define OP(i) asm volatile("v_mul_lo_u32 %0, %1, %2" : "=v"(a[i]) : "v"(a[i]), "s"(m));
     BODY8(OP)
 #undef OP
-  }
+  } T_END
   uint32_t s = 0;
   for (int i = 0; i < 8; ++i) s ^= a[i];
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
@@ -56,11 +72,11 @@ __global__ void k_mul_u24(uint32_t* out, uint32_t seed) {
   uint32_t a[8];
   uint32_t m = 0x511F53u ^ seed;
   for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
-  for (int it = 0; it < ITERS; ++it) {
+  T_BEGIN for (int it = 0; it < ITERS; ++it) {
 #define OP(i) asm volatile("v_mul_u32_u24 %0, %1, %2" : "=v"(a[i]) : "v"(a[i]), "s"(m));
     BODY8(OP)
 #undef OP
-  }
+  } T_END
   uint32_t s = 0;
   for (int i = 0; i < 8; ++i) s ^= a[i];
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
@@ -69,11 +85,11 @@ __global__ void k_xor(uint32_t* out, uint32_t seed) {
   uint32_t a[8];
   uint32_t m = 0xD2511F53u ^ seed;
   for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
-  for (int it = 0; it < ITERS; ++it) {
+  T_BEGIN for (int it = 0; it < ITERS; ++it) {
 #define OP(i) asm volatile("v_xor_b32 %0, %1, %2" : "=v"(a[i]) : "v"(a[i]), "s"(m));
     BODY8(OP)
 #undef OP
-  }
+  } T_END
   uint32_t s = 0;
   for (int i = 0; i < 8; ++i) s ^= a[i];
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
@@ -82,11 +98,11 @@ __global__ void k_fma(uint32_t* out, uint32_t seed) {
   float a[8];
   float m = 1.0000001f + (float)seed;
   for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
-  for (int it = 0; it < ITERS; ++it) {
+  T_BEGIN for (int it = 0; it < ITERS; ++it) {
 #define OP(i) asm volatile("v_fma_f32 %0, %1, %2, %1" : "=v"(a[i]) : "v"(a[i]), "s"(m));
     BODY8(OP)
 #undef OP
-  }
+  } T_END
   float s = 0;
   for (int i = 0; i < 8; ++i) s += a[i];
   out[blockIdx.x * blockDim.x + threadIdx.x] = __float_as_uint(s);
@@ -96,11 +112,11 @@ __global__ void k_pk_fma(uint32_t* out, uint32_t seed) {
   v2f a[8];
   v2f m = {1.0000001f + (float)seed, 1.0000002f};
   for (int i = 0; i < 8; ++i) a[i] = v2f{(float)threadIdx.x, (float)i};
-  for (int it = 0; it < ITERS; ++it) {
+  T_BEGIN for (int it = 0; it < ITERS; ++it) {
 #define OP(i) asm volatile("v_pk_fma_f32 %0, %1, %2, %1" : "=v"(a[i]) : "v"(a[i]), "v"(m));
     BODY8(OP)
 #undef OP
-  }
+  } T_END
   float s = 0;
   for (int i = 0; i < 8; ++i) s += a[i].x + a[i].y;
   out[blockIdx.x * blockDim.x + threadIdx.x] = __float_as_uint(s);
@@ -109,11 +125,11 @@ __global__ void k_fma64(uint32_t* out, uint32_t seed) {
   double a[8];
   double m = 1.0000001 + (double)seed;
   for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
-  for (int it = 0; it < ITERS; ++it) {
+  T_BEGIN for (int it = 0; it < ITERS; ++it) {
 #define OP(i) asm volatile("v_fma_f64 %0, %1, %2, %1" : "=v"(a[i]) : "v"(a[i]), "v"(m));
     BODY8(OP)
 #undef OP
-  }
+  } T_END
   double s = 0;
   for (int i = 0; i < 8; ++i) s += a[i];
   out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)s;
@@ -121,11 +137,11 @@ __global__ void k_fma64(uint32_t* out, uint32_t seed) {
 __global__ void k_rcp(uint32_t* out, uint32_t seed) {
   float a[8];
   for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i + 1 + seed;
-  for (int it = 0; it < ITERS; ++it) {
+  T_BEGIN for (int it = 0; it < ITERS; ++it) {
 #define OP(i) asm volatile("v_rcp_f32 %0, %1" : "=v"(a[i]) : "v"(a[i]));
     BODY8(OP)
 #undef OP
-  }
+  } T_END
   float s = 0;
   for (int i = 0; i < 8; ++i) s += a[i];
   out[blockIdx.x * blockDim.x + threadIdx.x] = __float_as_uint(s);
@@ -134,11 +150,11 @@ __global__ void k_cvt_f64(uint32_t* out, uint32_t seed) {
   double a[8];
   float f[8];
   for (int i = 0; i < 8; ++i) f[i] = threadIdx.x * 7 + i + 1 + seed;
-  for (int it = 0; it < ITERS; ++it) {
+  T_BEGIN for (int it = 0; it < ITERS; ++it) {
 #define OP(i) asm volatile("v_cvt_f64_f32 %0, %1" : "=v"(a[i]) : "v"(f[i]));
     BODY8(OP)
 #undef OP
-  }
+  } T_END
   double s = 0;
   for (int i = 0; i < 8; ++i) s += a[i];
   out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)s;
@@ -150,9 +166,9 @@ __global__ void k_cvt_f64(uint32_t* out, uint32_t seed) {
     T a[8];                                                                              \
     T m = (T)(1.0000001f + (float)seed);                                                 \
     for (int i = 0; i < 8; ++i) a[i] = (T)(threadIdx.x * 7 + i);                         \
-    for (int it = 0; it < ITERS; ++it) {                                                 \
+    T_BEGIN for (int it = 0; it < ITERS; ++it) {                                                 \
       OPS_##NAME                                                                         \
-    }                                                                                    \
+    } T_END                                                                                    \
     T s = 0;                                                                             \
     for (int i = 0; i < 8; ++i) s += a[i];                                               \
     out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)s;                            \
@@ -192,11 +208,11 @@ __global__ void k_cndmask_vcc(uint32_t* out, uint32_t seed) {
   uint32_t m = 0x12345u ^ seed;
   for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
   asm volatile("v_cmp_gt_u32 vcc, 32, %0" ::"v"(threadIdx.x) : "vcc");
-  for (int it = 0; it < ITERS; ++it) {
+  T_BEGIN for (int it = 0; it < ITERS; ++it) {
 #define OP(i) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a[i]) : "v"(m) : "vcc");
     BODY8(OP)
 #undef OP
-  }
+  } T_END
   uint32_t s = 0;
   for (int i = 0; i < 8; ++i) s ^= a[i];
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
@@ -207,11 +223,11 @@ __global__ void k_cndmask_sgpr(uint32_t* out, uint32_t seed) {
   for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
   unsigned long long msk;
   asm volatile("v_cmp_gt_u32 %0, 32, %1" : "=s"(msk) : "v"(threadIdx.x));
-  for (int it = 0; it < ITERS; ++it) {
+  T_BEGIN for (int it = 0; it < ITERS; ++it) {
 #define OP(i) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a[i]) : "v"(m), "s"(msk));
     BODY8(OP)
 #undef OP
-  }
+  } T_END
   uint32_t s = 0;
   for (int i = 0; i < 8; ++i) s ^= a[i];
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
@@ -220,14 +236,14 @@ __global__ void k_cndmask_sgpr(uint32_t* out, uint32_t seed) {
 __global__ void k_select_cc(uint32_t* out, uint32_t seed) {
   float a[8], b[8];
   for (int i = 0; i < 8; ++i) { a[i] = threadIdx.x * 7 + i; b[i] = (float)(seed + i); }
-  for (int it = 0; it < ITERS; ++it) {
+  T_BEGIN for (int it = 0; it < ITERS; ++it) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float t = b[i] * 1.0001f;
       a[i] = t < a[i] ? t : a[i];
       b[i] = t;
     }
-  }
+  } T_END
   float s = 0;
   for (int i = 0; i < 8; ++i) s += a[i] + b[i];
   out[blockIdx.x * blockDim.x + threadIdx.x] = __float_as_uint(s);
@@ -240,7 +256,7 @@ __global__ void k_select_cc(uint32_t* out, uint32_t seed) {
     T a[8];                                                                              \
     T m = (T)(1.0000001f + (float)seed);                                                 \
     for (int i = 0; i < 8; ++i) a[i] = (T)(threadIdx.x * 7 + i);                         \
-    for (int it = 0; it < ITERS; ++it) { CHS8(ASM) }                                     \
+    T_BEGIN for (int it = 0; it < ITERS; ++it) { CHS8(ASM) } T_END                                     \
     T s = 0;                                                                             \
     for (int i = 0; i < 8; ++i) s += a[i];                                               \
     out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)s;                            \
@@ -266,11 +282,11 @@ __global__ void k_lshl_add_u64(uint32_t* out, uint32_t seed) {
   uint64_t a[8];
   uint64_t m = 0x12345ull ^ seed;
   for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
-  for (int it = 0; it < ITERS; ++it) {
+  T_BEGIN for (int it = 0; it < ITERS; ++it) {
 #define OP(i) asm volatile("v_lshl_add_u64 %0, %0, 2, %1" : "+v"(a[i]) : "v"(m));
     BODY8(OP)
 #undef OP
-  }
+  } T_END
   uint64_t s = 0;
   for (int i = 0; i < 8; ++i) s ^= a[i];
   out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)s;
@@ -279,11 +295,11 @@ __global__ void k_mov_b64(uint32_t* out, uint32_t seed) {
   uint64_t a[8];
   uint64_t m = 0x12345ull ^ seed;
   for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
-  for (int it = 0; it < ITERS; ++it) {
+  T_BEGIN for (int it = 0; it < ITERS; ++it) {
 #define OP(i) asm volatile("v_mov_b64 %0, %1" : "=v"(a[i]) : "v"(m + i));
     BODY8(OP)
 #undef OP
-  }
+  } T_END
   uint64_t s = 0;
   for (int i = 0; i < 8; ++i) s ^= a[i];
   out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)s;
@@ -292,22 +308,22 @@ __global__ void k_readlane(uint32_t* out, uint32_t seed) {
   uint32_t a[8];
   for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i + seed;
   uint32_t acc = 0;
-  for (int it = 0; it < ITERS; ++it) {
+  T_BEGIN for (int it = 0; it < ITERS; ++it) {
 #define OP(i) { uint32_t r; asm volatile("v_readlane_b32 %0, %1, 3" : "=s"(r) : "v"(a[i])); acc += r; }
     BODY8(OP)
 #undef OP
-  }
+  } T_END
   out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
 }
 __global__ void k_writelane(uint32_t* out, uint32_t seed) {
   uint32_t a[8];
   for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
   uint32_t sv = seed;
-  for (int it = 0; it < ITERS; ++it) {
+  T_BEGIN for (int it = 0; it < ITERS; ++it) {
 #define OP(i) asm volatile("v_writelane_b32 %0, %1, 5" : "+v"(a[i]) : "s"(sv));
     BODY8(OP)
 #undef OP
-  }
+  } T_END
   uint32_t s = 0;
   for (int i = 0; i < 8; ++i) s ^= a[i];
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
@@ -344,10 +360,17 @@ static void run(const char* name, K k, uint32_t* d) {
     hipEventSynchronize(e1);
     float ms = 0;
     hipEventElapsedTime(&ms, e0, e1);
-    const double insts_per_simd = 5.0 * waves_per_simd * ITERS * 8;  // wave-instructions
-    const double cyc = ms * 1e-3 / 5.0 * 2.4e9;  // at 2.4 GHz nominal
-    printf("{\"instr\": \"%s\", \"waves_per_simd\": %d, \"cycles_per_wave_instr\": %.2f}\n", name,
-           waves_per_simd, cyc * 5.0 / insts_per_simd);
+    unsigned long long tim[2] = {0, 0};
+    hipMemcpyFromSymbol(tim, HIP_SYMBOL(g_tim), sizeof(tim));
+    const double insts_per_simd = (double)waves_per_simd * ITERS * 8;  // one launch
+    const double ghz = tim[1] ? (double)tim[0] / (double)tim[1] * 0.1 : 0.0;  // 100 MHz realtime
+    // wall clock at the measured frequency (the old method, at 2.4 GHz nominal, beside it)
+    const double cyc_wall = ms * 1e-3 / 5.0 * ghz * 1e9;
+    printf("{\"instr\": \"%s\", \"waves_per_simd\": %d, \"cycles_per_wave_instr\": %.3f, "
+           "\"cycles_per_wave_instr_wall\": %.3f, \"cycles_per_wave_instr_wall_2p4\": %.3f, "
+           "\"shader_ghz\": %.3f}\n",
+           name, waves_per_simd, (double)tim[0] / insts_per_simd, cyc_wall / insts_per_simd,
+           ms * 1e-3 / 5.0 * 2.4e9 / insts_per_simd, ghz);
   }
 }
 

@@ -17,7 +17,7 @@ rt.tune_from_env()  # dev tool: RT_* knobs from the environment (rt_tune_set)
 
 NAMES = ["grab", "trav", "media", "shade", "tex", "light", "term", "loop",
          "trav_lanes", "trav_rounds", "shade_lanes", "shade_rounds", "step_lanes", "step_wave",
-         "qnode_lanes", "qleaf_lanes", "qmixed", "qiters"]
+         "qnode_lanes", "qleaf_lanes", "qmixed", "qiters", "qsame", "quniq", "qtop", "qmid"]
 scene, width, spp = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
 t, cam, w, l = rt.demo_scene(scene)
 cam.Width = width
@@ -32,7 +32,7 @@ with rt.Scene(t, w, l) as sc:
     kw = {"chunk": int(os.environ["CHUNK"])} if "CHUNK" in os.environ else {}
     img, st = sc.render(cam, profile=True, nranks=int(os.environ.get("NRANKS", "1")), **kw)
     rt.untune("RT_WAVE_TIMES")
-a = np.fromfile(path, dtype=np.uint64).reshape(-1, 22).astype(np.float64)
+a = np.fromfile(path, dtype=np.uint64).reshape(-1, 4 + len(NAMES)).astype(np.float64)
 ph = a[:, 4:].sum(axis=0)
 loop = ph[7]
 out = {"scene": scene, "W": width, "spp": spp, "ms": round(st["ms_fused"], 2),
@@ -51,4 +51,9 @@ if ph[17] > 0:  # compressed-BVH kernels: node / leaf lanes per iteration, mixed
     out["q_node_lanes_per_iter"] = round(ph[14] / ph[17], 2)
     out["q_leaf_lanes_per_iter"] = round(ph[15] / ph[17], 2)
     out["q_mixed_iter_frac"] = round(ph[16] / ph[17], 4)
+    lanes = ph[14] + ph[15]
+    out["q_lanes_on_first_item"] = round(ph[18] / lanes, 4)  # scalar-fetch candidates
+    out["q_distinct_items_per_iter"] = round(ph[19] / ph[17], 2)
+    out["q_lanes_levels_0_3"] = round(ph[20] / lanes, 4)
+    out["q_lanes_levels_4_5"] = round(ph[21] / lanes, 4)
 print(json.dumps(out), flush=True)

@@ -21,7 +21,7 @@ with rt.Scene(t, w, l) as sc:
         rt.tune("RT_WAVE_TIMES", path)
         img, st = sc.render(cam, nranks=n, profile=True)
         rt.untune("RT_WAVE_TIMES")
-        a = np.fromfile(path, dtype=np.uint64).reshape(-1, 22).astype(np.int64)
+        a = np.fromfile(path, dtype=np.uint64).reshape(-1, 26).astype(np.int64)
         t0 = a[:, 0].min()
         start = (a[:, 0] - t0) / 100.0  # 100 MHz -> µs
         end = (a[:, 1] - t0) / 100.0
