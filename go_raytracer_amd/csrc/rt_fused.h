@@ -247,6 +247,9 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
       if constexpr (kSplit)
         if (j0) s.flags = F_SPLIT | (n0 << kCountShift);
       trav_init<FT>(P.sc, s.o, s.d, s.time, tr);
+#ifdef RT_QROOT  // (opt-in: +2-4 % on C3-C5)
+      if constexpr (TREE == 5) trav_root_q(ts, s.o, 0.001f, tr);
+#endif
       has = true;
     }
     PH_ADD(PH_GRAB, t_grab);
@@ -320,7 +323,12 @@ __global__ __launch_bounds__(256, fused_waves(FT, TREE)) void k_fused(Params P) 
 #endif
         PH_T(t_shade);
         if (shade_core<false, FT>(P, slot, s, best, ws, sa) == OUT_NEED_CHUNK) has = false;
-        else trav_init<FT>(P.sc, s.o, s.d, s.time, tr);
+        else {
+          trav_init<FT>(P.sc, s.o, s.d, s.time, tr);
+#ifdef RT_QROOT  // (opt-in: +2-4 % on C3-C5)
+          if constexpr (TREE == 5) trav_root_q(ts, s.o, 0.001f, tr);
+#endif
+        }
         PH_ADD(PH_SHADE, t_shade);
       }
     }

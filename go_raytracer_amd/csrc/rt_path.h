@@ -149,6 +149,10 @@ RT_D void st_glb(F4* p, F4 v) { *(glb_v4*)p = v4f{v.x, v.y, v.z, v.w}; }
 // v_cmp + v_cndmask, both of which issue at half rate or less on gfx950
 // (profiles/r4_instr_rate.jsonl)
 RT_D uint32_t pick_by(uint32_t a, uint32_t b, uint32_t m) { return __builtin_amdgcn_bitop3_b32(a, b, m, 0xD8); }
+// a & ~m as one v_bitop3 (written as `a & ~m` with m a spread sign, LLVM turns it into a
+// compare and a v_cndmask_b32_e32 on vcc, which issues at ~23 cycles per wave64 on gfx950
+// whatever the occupancy: tools/instr_rate.hip, profiles/r6_instr_rate.jsonl)
+RT_D uint32_t and_not(uint32_t a, uint32_t m) { return __builtin_amdgcn_bitop3_b32(a, m, 0u, 0x30); }
 // all ones when x < 0 (sign bit set), else 0: -0 and negative NaNs count as negative
 RT_D uint32_t neg_mask(float x) { return (uint32_t)((int32_t)__float_as_uint(x) >> 31); }
 RT_D uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
@@ -527,6 +531,34 @@ RT_D void qnode_children(const F4 v[4], f3 o, f3 inv, float tmin, float tmax, fl
   cx(0, 2);
   cx(1, 3);
   cx(1, 2);
+}
+
+// The compressed BVH4's root tested where a ray starts (trav_init), from scalar loads: every
+// lane reads the same 64-B item 0, so s_load_dwordx4 x 4 through the scalar cache instead of
+// one of the ~8 vector-memory steps per segment (C5's traversal is bound by the vector-memory
+// path), and the traversal begins at the nearest child with the others on the
+// stack, exactly as the step would have left it (same qnode_children arithmetic: same image).
+RT_D void trav_root_q(const TravStack& stack, f3 o, float tmin, Trav& tr) {
+  if (tr.cur != 0u) return;  // item 0 is the root (render_impl, tree 5)
+  const F4* rn = kparams()->sc.nodes;
+  const F4 v[4] = {ld_cst(rn), ld_cst(rn + 1), ld_cst(rn + 2), ld_cst(rn + 3)};
+  float tn[4];
+  uint32_t ch[4];
+  qnode_children(v, o, tr.inv, tmin, tr.best.t, tn, ch);
+  if (tn[0] == kInf) {
+    tr.cur = TRAV_DONE;
+    return;
+  }
+  lds_u32* q = (lds_u32*)stack.lds;  // sp = 0: entries 0-2 are in the short stack
+  int sp = 0;
+  q[sp * 256] = ch[3];
+  sp += tn[3] != kInf;
+  q[sp * 256] = ch[2];
+  sp += tn[2] != kInf;
+  q[sp * 256] = ch[1];
+  sp += tn[1] != kInf;
+  tr.sp = sp;
+  tr.cur = ch[0];
 }
 
 // QN: the compressed BVH4 (host_qbvh.cpp, rt_device.h "compressed BVH4 node"), 64-B
@@ -1081,7 +1113,9 @@ RT_D void brute_axis(const DevScene& sc, const F4* lrec, int p0, int p1, const v
                      const v2f* Dv, float tmin, float& best, uint32_t& bk) {
   constexpr int B0 = AX == 0 ? 1 : 0, B1 = AX == 2 ? 1 : 2;  // in-plane axes, ascending
   const float da = Dv[AX].x;
-  const float ia = fabsf(da) >= 1e-8f ? rcp(da) : __builtin_nanf("");  // |n.d| < 1e-8: no hit
+  // |n.d| < 1e-8: no hit (NaN), as a sign-mask select (a compare and v_cndmask_b32_e32 on
+  // vcc cost ~23 cycles, and_not above)
+  const float ia = bitsf(pick_by(fbits(rcp(da)), 0x7FC00000u, neg_mask(fabsf(da) - 1e-8f)));
   const v2f inv = {ia, ia};
   for (int p = p0; p < p1; ++p) {
     v4f r[7];
@@ -1111,7 +1145,9 @@ template <int A, int H>
 RT_D void brute_half(const v4f* r, f3 o, f3 d, float tmin, float& best, uint32_t& bk) {
   constexpr int B0 = A == 0 ? 1 : 0, B1 = A == 2 ? 1 : 2;  // in-plane axes, ascending
   const float da = comp<A>(d);
-  const float ia = fabsf(da) >= 1e-8f ? rcp(da) : __builtin_nanf("");  // |n.d| < 1e-8: no hit
+  // |n.d| < 1e-8: no hit (NaN), as a sign-mask select (a compare and v_cndmask_b32_e32 on
+  // vcc cost ~23 cycles, and_not above)
+  const float ia = bitsf(pick_by(fbits(rcp(da)), 0x7FC00000u, neg_mask(fabsf(da) - 1e-8f)));
   const float t = ((H ? r[1].w : r[1].z) - comp<A>(o)) * ia;
   const float pb = fmaf(comp<B0>(d), t, comp<B0>(o)) - (H ? pair_q<B0>(r).y : pair_q<B0>(r).x);
   const float pc = fmaf(comp<B1>(d), t, comp<B1>(o)) - (H ? pair_q<B1>(r).y : pair_q<B1>(r).x);
@@ -1528,8 +1564,10 @@ RT_D f3 tex_value(const DevScene& sc, int tex, float u, float v, f3 p) {
     if (HAS(FT_IMAGE) && (!HAS(FT_NOISE) || T.kind == RT_TEX_IMAGE)) {  // texture.go:70-86 + PixelData imageLoader.go:52-62
       const DevImage im = sc.images[T.a];
       if (im.h <= 0) return mk3(0, 1, 1);
-      float uu = fabsf(fmodf(u, 1.0f));
-      float vv = 1.0f - fabsf(fmodf(v, 1.0f));
+      // fmod(u, 1) is u - trunc(u) exactly (no rounding for any finite u; inf and NaN give
+      // NaN either way), without the library fmodf's loop and selects
+      float uu = fabsf(u - truncf(u));
+      float vv = 1.0f - fabsf(v - truncf(v));
       float fi = uu * (float)(im.w - 1), fj = vv * (float)(im.h - 1);
       int i = isnan(fi) ? 0 : (int)fi, j = isnan(fj) ? 0 : (int)fj;
       i = min(max(i, 0), im.w);
@@ -1609,7 +1647,7 @@ RT_D float prim_pdf(const DevScene& sc, uint32_t ref, int li, f3 origin, f3 dir)
   // dist2 / (cosine * area) with dist2 = t^2 |dir|^2, cosine = |dir.n| / |dir|; +0 on a
   // miss (the mask clears every bit of whatever the missed test's t gave)
   const float dd = dot(dir, dir);
-  return bitsf(fbits((t * t * dd) * fsqrt(dd) * rcp(fabsf(dot(dir, n)) * area)) & ~miss);
+  return bitsf(and_not(fbits((t * t * dd) * fsqrt(dd) * rcp(fabsf(dot(dir, n)) * area)), miss));
 }
 
 // HittableList.PdfValue hittable.go:89-97 over the flattened light table
@@ -2187,7 +2225,11 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
         if (!cannot) {
           float r0 = (1.0f - ior) * rcp(1.0f + ior);
           r0 = r0 * r0;
-          float refl_p = r0 + (1.0f - r0) * powf(1.0f - cs, 5.0f);
+          // Schlick's (1 - cos)^5 (materials.go:132-136, math.Pow) as three multiplies: the
+          // library powf is ~40 instructions with its special-case selects; the product is
+          // within a few ulp of it for the base in [0, 1]
+          const float x = 1.0f - cs, x2 = x * x;
+          float refl_p = r0 + (1.0f - r0) * (x2 * x2 * x);
           refl = refl_p > rt_unit_f(r.v[0]);
         }
         ndir = refl ? reflect(ud, n) : refract(ud, n, ri);
@@ -2215,7 +2257,7 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
           f3 ud = unit(ndir);
           bsdf_pdf = fmaxf(0.0f, dot(ud, b.w) * kInvPi);  // 1 ulp of /pi, no division sequence
           float ct = dot(n, ud);
-          spdf = ct < 0.0f ? 0.0f : ct * kInvPi;
+          spdf = fmaxf(0.0f, ct * kInvPi);  // (kInvPi > 0: zero exactly when ct < 0)
         }
 #ifdef ABL_NO_LIGHTPDF
         float pdf = 0.5f * 0.01f + 0.5f * bsdf_pdf;  // ablation build (timing only)
@@ -2323,7 +2365,9 @@ RT_D int shade_core(const Params& P, uint32_t slot, Path& s, const Hit& h, const
       maxI = L.x + L.y + L.z;
       ws.fold_max(P, slot, s.nst, L, maxI);
     }
-    if (maxI > P.maxc) L = L * (P.maxc * rcp(maxI));
+    // min(1, M / maxI) as one v_min: no compare and three v_cndmask_b32_e32 (and_not); the
+    // scale is exactly 1 whenever M * rcp(maxI) >= 1 (maxI below M by more than an ulp)
+    L = L * fminf(1.0f, P.maxc * rcp(maxI));
 #endif
     if (s.flags & F_PRE) L = get_pre<SOA>(P, slot, s) * L;
   } else {

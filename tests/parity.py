@@ -45,17 +45,18 @@ P1_BAR = 0.995
 
 # >= 99.5 % of linear-RGB channels within 2^-10 * max(1, |ref|)
 # ("frac_close") and of 8-bit outputs equal ("q_equal").  Every scene is held to it
-# except the two named here, each with its measured GPU result (round 5,
-# profiles/r5_parity_final.jsonl):
-# on these the paths are chaotic and fp32 and fp64 paths fork after a few bounces
-# whatever the implementation (tools/fork_probe.py).
+# except the one named here, with its measured GPU result (round 6,
+# profiles/r6_parity_final.jsonl): its paths are chaotic, and fp32 and fp64 paths fork after
+# a few bounces whatever the implementation (tools/fork_census.py: 168 of 196 forked samples
+# part at the 4th vertex or later, none at the camera ray).
+# (Round 6: the `cluster` feature scene, 200 small spheres, renders at 64 x 64 x 32 and meets
+# P1 itself, q_equal 0.9990 against 0.995 on 12,288 channels, ~14 sigma; at 32 x 32 x 16 it
+# had needed its own 0.990 bar.)
 P1_EXCEPTIONS = {
-    # the 200-small-spheres feature scene: q_equal fused 0.9941, wavefront 0.9912
-    # (frac_close 0.9990 meets P1)
-    "cluster": {"q_equal": 0.990},
-    # C5, the 1M-triangle metal knot at 1920x1080x1024 (row subsample):
-    # frac_close 0.9933 / 0.9931, q_equal 0.9914 / 0.9916 on the two row sets (compressed
-    # BVH4, surface projection; round 4: 0.9946 / 0.9927)
+    # C5, the 1M-triangle metal knot at 1920x1080x1024 (row subsample, 17 rows each):
+    # frac_close 0.99315 / 0.99314, q_equal 0.99146 / 0.99175 on the two row sets (round 5:
+    # 0.9933 / 0.9931 and 0.9914 / 0.9916).  The GPU render and the oracle are deterministic,
+    # so the margin does not vary from box to box; it moves only with the arithmetic.
     "model": {"frac_close": 0.993, "q_equal": 0.990},
 }
 

@@ -1,9 +1,9 @@
 """Per-feature GPU-vs-oracle parity: one small scene per reference feature.
 
 Tolerance: >= 99.5 % of linear-RGB channels within
-2^-10 * max(1, |ref|) and of 8-bit outputs equal, for every feature scene except the
-one named exception in tests/parity.py P1_EXCEPTIONS (`cluster`, 200 small spheres:
-8-bit equality >= 0.990, measured 0.9941 fused / 0.9922 wavefront).  The oracle's fp32
+2^-10 * max(1, |ref|) and of 8-bit outputs equal, for every feature scene (round 6: the
+`cluster` scene renders at 64 x 64 x 32 and no longer needs its own bar; measured 8-bit
+equality 0.9990 fused and wavefront, profiles/r6_parity_final.jsonl).  The oracle's fp32
 twin (the reference's algorithm evaluated in float) is rendered on the same pixels and
 logged next to the GPU's numbers (PARITY_LOG) for information only; it sets no bar.
 """

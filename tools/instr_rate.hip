@@ -1,8 +1,9 @@
 // Issue cost of the integer and fp ops the path tracer's RNG and traversal use (dev tool):
 // hipcc --offload-arch=gfx950 -O3 tools/instr_rate.hip -o /tmp/instr_rate && /tmp/instr_rate
-// Each kernel runs 8 independent chains of one instruction per lane for ITERS iterations;
-// the result is SIMD cycles per wave-instruction, at 1 wave per SIMD and at 8 waves per SIMD
-// (the device-wide throughput: elapsed clock x SIMDs / instructions issued).
+// Each kernel runs 8 independent chains of one instruction per lane for ITERS iterations (the
+// loop unrolled 8x: 64 instructions per 3 SALU of loop control); the result is SIMD cycles
+// per wave-instruction at 1, 2 and 4 waves per SIMD, from the launch's wall time at the
+// shader clock measured in the kernel (one block per CU: see run()).
 #include <hip/hip_runtime.h>
 #pragma clang diagnostic ignored "-Wunused-value"
 #pragma clang diagnostic ignored "-Wunused-result"
@@ -232,6 +233,107 @@ __global__ void k_cndmask_sgpr(uint32_t* out, uint32_t seed) {
   for (int i = 0; i < 8; ++i) s ^= a[i];
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
+// the same select as VOP3 (e64) naming vcc, and VOP2 after a scalar write of vcc: is the
+// ~23-cycle cost of v_cndmask_b32_e32 the encoding or the implicit vcc read?
+__global__ void k_cndmask_e64_vcc(uint32_t* out, uint32_t seed) {
+  uint32_t a[8];
+  uint32_t m = 0x12345u ^ seed;
+  for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
+  asm volatile("v_cmp_gt_u32 vcc, 32, %0" ::"v"(threadIdx.x) : "vcc");
+  T_BEGIN for (int it = 0; it < ITERS; ++it) {
+#define OP(i) asm volatile("v_cndmask_b32_e64 %0, %0, %1, vcc" : "+v"(a[i]) : "v"(m) : "vcc");
+    BODY8(OP)
+#undef OP
+  } T_END
+  uint32_t s = 0;
+  for (int i = 0; i < 8; ++i) s ^= a[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+__global__ void k_cndmask_vcc_salu(uint32_t* out, uint32_t seed) {
+  uint32_t a[8];
+  uint32_t m = 0x12345u ^ seed;
+  for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
+  asm volatile("s_mov_b64 vcc, 0x5555" ::: "vcc");
+  T_BEGIN for (int it = 0; it < ITERS; ++it) {
+#define OP(i) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a[i]) : "v"(m) : "vcc");
+    BODY8(OP)
+#undef OP
+  } T_END
+  uint32_t s = 0;
+  for (int i = 0; i < 8; ++i) s ^= a[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+// one VOP2 select on vcc after three independent adds (how a compiled kernel meets them)
+__global__ void k_cndmask_mixed(uint32_t* out, uint32_t seed) {
+  uint32_t a[8];
+  float f[8];
+  uint32_t m = 0x12345u ^ seed;
+  for (int i = 0; i < 8; ++i) { a[i] = threadIdx.x * 7 + i; f[i] = (float)i; }
+  asm volatile("v_cmp_gt_u32 vcc, 32, %0" ::"v"(threadIdx.x) : "vcc");
+  T_BEGIN for (int it = 0; it < ITERS; ++it) {
+#define OP(i) asm volatile("v_add_f32 %0, %0, %0\n\tv_add_f32 %0, %0, %0\n\tv_add_f32 %0, %0, %0\n\t" \
+                           "v_cndmask_b32 %1, %1, %2, vcc" : "+v"(f[i]), "+v"(a[i]) : "v"(m) : "vcc");
+    BODY8(OP)
+#undef OP
+  } T_END
+  uint32_t s = 0;
+  for (int i = 0; i < 8; ++i) s ^= a[i] ^ __float_as_uint(f[i]);
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+// VOP2 select right after the VALU compare that writes vcc (the compiler's pattern), and after
+// an SALU write of vcc (s_and_b64 vcc, s, vcc: the compiler's pattern for a select under a
+// branch condition)
+__global__ void k_cmp_cndmask(uint32_t* out, uint32_t seed) {
+  uint32_t a[8];
+  uint32_t m = 0x12345u ^ seed;
+  for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
+  T_BEGIN for (int it = 0; it < ITERS; ++it) {
+#define OP(i) asm volatile("v_cmp_gt_u32 vcc, %0, %1\n\ts_nop 1\n\tv_cndmask_b32 %0, %0, %1, vcc" \
+                           : "+v"(a[i]) : "v"(m) : "vcc");
+    BODY8(OP)
+#undef OP
+  } T_END
+  uint32_t s = 0;
+  for (int i = 0; i < 8; ++i) s ^= a[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+__global__ void k_sand_cndmask(uint32_t* out, uint32_t seed) {
+  uint32_t a[8];
+  uint32_t m = 0x12345u ^ seed;
+  for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
+  unsigned long long msk;
+  asm volatile("v_cmp_gt_u32 %0, 32, %1" : "=s"(msk) : "v"(threadIdx.x));
+  T_BEGIN for (int it = 0; it < ITERS; ++it) {
+#define OP(i) asm volatile("s_and_b64 vcc, %2, exec\n\tv_cndmask_b32 %0, %0, %1, vcc" \
+                           : "+v"(a[i]) : "v"(m), "s"(msk) : "vcc", "scc");
+    BODY8(OP)
+#undef OP
+  } T_END
+  uint32_t s = 0;
+  for (int i = 0; i < 8; ++i) s ^= a[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+// v_add_f32 as ONE asm statement of 64 instructions per loop trip: the compiler puts an
+// s_nop 0 between consecutive asm statements (it cannot see their hazards), so the 8-per-
+// statement kernels above issue 9 instructions per 8 adds; here 1 per 64
+#define ADD8 "v_add_f32 %0, %0, %8\n\t""v_add_f32 %1, %1, %8\n\t""v_add_f32 %2, %2, %8\n\t""v_add_f32 %3, %3, %8\n\t""v_add_f32 %4, %4, %8\n\t""v_add_f32 %5, %5, %8\n\t""v_add_f32 %6, %6, %8\n\t""v_add_f32 %7, %7, %8\n\t"
+__global__ void k_add_f32_asm64(uint32_t* out, uint32_t seed) {
+  float a[8];
+  float m = 1.0000001f + (float)seed;
+  for (int i = 0; i < 8; ++i) a[i] = threadIdx.x * 7 + i;
+  T_BEGIN for (int it = 0; it < ITERS; it += 8) {
+    asm volatile(ADD8 ADD8 ADD8 ADD8 ADD8 ADD8 ADD8 ADD8
+                 : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]),
+                   "+v"(a[6]), "+v"(a[7])
+                 : "v"(m));
+  } T_END
+  float s = 0;
+  for (int i = 0; i < 8; ++i) s += a[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = __float_as_uint(s);
+}
+
 // compiler-generated selects: x = c ? y : x with c from a float compare each iteration
 __global__ void k_select_cc(uint32_t* out, uint32_t seed) {
   float a[8], b[8];
@@ -351,32 +453,45 @@ static void run(const char* name, K k, uint32_t* d) {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  for (int waves_per_simd : {1, 2, 4, 8}) {
-    const int blocks = cus * waves_per_simd;  // 256-thread blocks: one wave per SIMD each
-    hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, 0, d, 1u);
+  // ONE block per CU (96 KiB of dynamic LDS each: two never fit the CU's 160 KiB), of w waves
+  // per SIMD (64 x 4 x w threads): every SIMD then runs exactly w waves, so the kernel's
+  // time is w x the per-wave instruction count at the SIMD's issue rate.  (Round 4's version
+  // launched cus x w blocks of 256 threads and let the dispatcher place them: an uneven
+  // placement puts w + 1 waves on some SIMDs and inflates every rate by up to ~20 %.)
+  const size_t lds = 96 * 1024;
+  hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  for (int waves_per_simd : {1, 2, 4}) {
+    const int threads = 256 * waves_per_simd;
+    hipLaunchKernelGGL(k, dim3(cus), dim3(threads), lds, 0, d, 1u);
     hipEventRecord(e0);
-    for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, 0, d, 1u);
+    for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(k, dim3(cus), dim3(threads), lds, 0, d, 1u);
     hipEventRecord(e1);
     hipEventSynchronize(e1);
+    if (hipGetLastError() != hipSuccess) {
+      printf("{\"instr\": \"%s\", \"error\": \"launch\"}\n", name);
+      continue;
+    }
     float ms = 0;
     hipEventElapsedTime(&ms, e0, e1);
     unsigned long long tim[2] = {0, 0};
     hipMemcpyFromSymbol(tim, HIP_SYMBOL(g_tim), sizeof(tim));
     const double insts_per_simd = (double)waves_per_simd * ITERS * 8;  // one launch
     const double ghz = tim[1] ? (double)tim[0] / (double)tim[1] * 0.1 : 0.0;  // 100 MHz realtime
-    // wall clock at the measured frequency (the old method, at 2.4 GHz nominal, beside it)
-    const double cyc_wall = ms * 1e-3 / 5.0 * ghz * 1e9;
+    // SIMD cycles per wave-instruction: the launch's wall time at the measured shader clock
+    // (one wave's s_memtime / s_memrealtime ratio; the oldest wave of a SIMD issues first,
+    // so its own elapsed cycles are not the SIMD's rate)
+    const double cyc = ms * 1e-3 / 5.0 * ghz * 1e9;
     printf("{\"instr\": \"%s\", \"waves_per_simd\": %d, \"cycles_per_wave_instr\": %.3f, "
-           "\"cycles_per_wave_instr_wall\": %.3f, \"cycles_per_wave_instr_wall_2p4\": %.3f, "
+           "\"cycles_per_wave_instr_at_2p4\": %.3f, \"oldest_wave_cycles_per_instr\": %.3f, "
            "\"shader_ghz\": %.3f}\n",
-           name, waves_per_simd, (double)tim[0] / insts_per_simd, cyc_wall / insts_per_simd,
-           ms * 1e-3 / 5.0 * 2.4e9 / insts_per_simd, ghz);
+           name, waves_per_simd, cyc / insts_per_simd, ms * 1e-3 / 5.0 * 2.4e9 / insts_per_simd,
+           (double)tim[0] / ((double)ITERS * 8), ghz);
   }
 }
 
 int main() {
   uint32_t* d;
-  hipMalloc(&d, 256 * 2048 * sizeof(uint32_t));
+  hipMalloc(&d, 256 * 2048 * sizeof(uint32_t));  // cus x 1024 threads
   run("v_mad_u64_u32", k_mad_u64, d);
   run("v_mul_hi_u32", k_mul_hi, d);
   run("v_mul_lo_u32", k_mul_lo, d);
@@ -388,6 +503,7 @@ int main() {
   run("v_rcp_f32", k_rcp, d);
   run("v_cvt_f64_f32", k_cvt_f64, d);
   run("v_add_f32", k_add_f32, d);
+  run("v_add_f32 (64 per asm statement, no s_nop)", k_add_f32_asm64, d);
   run("v_mul_f32", k_mul_f32, d);
   run("v_max_f32", k_max_f32, d);
   run("v_min3_f32", k_min3_f32, d);
@@ -402,6 +518,11 @@ int main() {
   run("v_cmp_lt_f32", k_cmp_f32, d);
   run("v_cndmask_b32 (vcc set once)", k_cndmask_vcc, d);
   run("v_cndmask_b32_e64 (sgpr mask)", k_cndmask_sgpr, d);
+  run("v_cndmask_b32_e64 (vcc mask)", k_cndmask_e64_vcc, d);
+  run("v_cndmask_b32 (vcc written by s_mov)", k_cndmask_vcc_salu, d);
+  run("3 v_add_f32 + 1 v_cndmask_b32 (vcc): per 4 instructions", k_cndmask_mixed, d);
+  run("v_cmp_gt_u32 vcc + s_nop 1 + v_cndmask_b32 (vcc): per pair", k_cmp_cndmask, d);
+  run("s_and_b64 vcc + v_cndmask_b32 (vcc): per pair", k_sand_cndmask, d);
   run("compiled select: mul + cmp + cndmask per element", k_select_cc, d);
   run("v_xor_b32_e64 (sgpr operand)", k_xor_vs, d);
   run("v_xor_b32 (vgpr operands)", k_xor_vv, d);
