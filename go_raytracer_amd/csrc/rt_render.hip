@@ -1030,9 +1030,17 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   const size_t node_slots = w4 ? 2 : 1;  // 64-B LDS slots per node
   const bool f_lds = node_slots * n_nodes <= lds_slots && !brute_smem;
   // the record loop's pairs, then (lean set) the quads' shade table, 4 F4 per 64-B slot
-  const bool shade_tab = tree == 0 && ft_set == 0u && ds->shade_n > 0;
+  // The record-loop LDS kernel reads its records from LDS only (trav_brute<.., SMEM = false>),
+  // so with a tree 0 in LDS the records must be staged: brute_smem above guarantees they fit
+  // alone, and a shade table that would push them over the budget is left out (the lean
+  // kernel then shades from the quad table in HBM).  Found in round 6: a 7-wave build shrank
+  // the budget below Cornell's records + table, and the kernel read unstaged LDS.
+  bool shade_tab = tree == 0 && ft_set == 0u && ds->shade_n > 0;
+  if (shade_tab && f_lds && brute_slots + (size_t)(ds->shade_n + 3) / 4 > lds_slots) shade_tab = false;
   const size_t rec_slots = tree == 0 ? brute_slots + (shade_tab ? (size_t)(ds->shade_n + 3) / 4 : 0) : n_refs;
   const bool f_recs = f_lds && node_slots * n_nodes + rec_slots <= lds_slots;
+  if (tree == 0 && f_lds && !f_recs)
+    return set_error(RT_ERR_UNSUPPORTED, "internal: record loop in LDS without its records");
   // Trees read through L1/L2 take the BVH8 (host_bvh8.cpp) when the scene has one (built
   // only with RT_BVH8=1) and a kernel exists for its feature set; RT_TREE=4 keeps the BVH4
   if (mode == RT_MODE_FUSED && tree == 4 && !f_lds && !s->h.nodes8.empty() && env_tree != 4 &&

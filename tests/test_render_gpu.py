@@ -465,3 +465,26 @@ def test_compressed_bvh_renders_like_bvh4(rt, gpu, tune, name, width, spp):
     assert [s["tree_width"] for s in sts] == [5, 4]
     assert np.array_equal(imgs[0], imgs[1], equal_nan=True)
     assert sts[0]["segments"] == sts[1]["segments"]
+
+
+@pytest.mark.parametrize("n_extra", [20, 23, 31])
+def test_record_loop_lds_budget_with_shade_table(rt, oracle, gpu, n_extra):
+    """The record-loop kernel with its records in LDS reads them from LDS only, so a scene
+    whose records fit the LDS budget but whose records + lean shade table do not must drop
+    the table, not the records (rt_render.hip, round 6: read unstaged, the kernel shaded
+    garbage quad indices and faulted).  The room's 3 quads + n_extra small tilted quads:
+    23-34 records at 6 waves per SIMD (34 LDS slots of 64 B) sit in that window."""
+    from tests import scenes
+    t = rt.Tree(5)
+    world, lights = scenes._room(t)
+    grey = t.lambertian((0.6, 0.5, 0.4))
+    for i in range(n_extra):
+        x, z = -6 + (i % 6) * 2.3, -3 + (i // 6) * 1.7
+        t.add(world, t.quad((x, 0.5 + 0.1 * i, z), (0.9, 0.3, 0.1), (0.1, 1.1, 0.4), grey))
+    cam = scenes._cam(rt, (0, 4, -14), (0, 2, 0), width=48, spp=16)
+    with rt.Scene(t, world, lights) as sc:
+        img, st = sc.render(cam, seed=4)
+    assert st["tree_width"] == 0  # the record loop
+    ref, _ = oracle.render(t, world, lights, cam, seed=4, threads=8)
+    m = compare(img, ref)
+    assert m["frac_close"] >= 0.995 and m["q_equal"] >= 0.995, m
