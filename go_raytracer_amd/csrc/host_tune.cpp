@@ -60,6 +60,7 @@ constexpr Knob kKnobs[] = {
     {"RT_CSUM", false, 'i', 0, 1},            // 0: pixel atomics instead of per-chunk records
     {"RT_CSUM_MAX_MB", false, 'i', 0, 16777216},     // per-chunk record buffer cap (MiB)
     {"RT_CHUNK_ROWS", false, 'i', -1, 1073741824},      // rows per chunk-order group
+    {"RT_SWEEP", false, 's', 0, 0},           // chunk-group sweep order: forward | reverse
     {"RT_STEP_BUDGET", false, 'i', 1, 1073741824},     // traversal steps per scheduling round
     {"RT_SHADE_MIN", false, 'i', 1, 64},       // ready lanes before a wave shades
     {"RT_GRAB_MIN", false, 'i', 1, 1048576},        // chunks per refill of a wave's batch
@@ -132,6 +133,9 @@ int rt_tune_set(const char* name, const char* value) {
       strcmp(value, "device") != 0 && strcmp(value, "auto") != 0 && value[0] != '\0')
     return rt::set_error(RT_ERR_INVALID, "rt_tune_set: RT_BVH_BUILDER=\"%s\" (host | device | auto)",
                          value);
+  if (value && strcmp(name, "RT_SWEEP") == 0 && strcmp(value, "forward") != 0 &&
+      strcmp(value, "reverse") != 0 && value[0] != '\0')
+    return rt::set_error(RT_ERR_INVALID, "rt_tune_set: RT_SWEEP=\"%s\" (forward | reverse)", value);
   std::lock_guard<std::mutex> lk(rt::g_mu);
   if (value) rt::g_set[name] = value;
   else rt::g_set.erase(name);

@@ -62,6 +62,10 @@ struct Params {
   FastDiv fd_width, fd_s;
   FastDiv fd_gchunks, fd_gpix;  // chunk order: groups of fd_gpix.d pixels x all sample blocks
   FastDiv fd_gchunks2;          // the tail phase's chunks per group (gpix x its blocks)
+#ifdef RT_SWEEP_ORDER
+  uint32_t gflip, gbase;        // group at sweep position q: (q ^ gflip) + gbase (0, 0: image
+                                // order; ~0, groups: reversed, RT_SWEEP) -- and back (k_resolve)
+#endif
   // camera (initialize camera.go:179-253, converted to fp32)
   float p00r[3], du[3], dv[3], cc[3], dku[3], dkv[3];  // p00r = pixel00 - center
   float bg[3];
@@ -229,8 +233,13 @@ RT_D uint32_t chunk_pixel(const Params& P, uint32_t chunk, uint32_t& sub) {
   const FastDiv fg = tail ? FastDiv{kp->fd_gchunks2.m, kp->fd_gchunks2.s1, kp->fd_gchunks2.s2,
                                     kp->fd_gchunks2.d}
                           : P.fd_gchunks;
-  const uint32_t q = fdiv(c, fg);
-  const uint32_t r = c - q * fg.d;
+  const uint32_t qs = fdiv(c, fg);
+  const uint32_t r = c - qs * fg.d;
+#ifdef RT_SWEEP_ORDER  // (opt-in build: RT_SWEEP=reverse, DESIGN.md §8 "Sweep order")
+  const uint32_t q = (qs ^ kp->gflip) + kp->gbase;  // the group at this sweep position
+#else
+  const uint32_t q = qs;
+#endif
   sub = fdiv(r, P.fd_gpix);
   return q * P.fd_gpix.d + (r - sub * P.fd_gpix.d);
 }
@@ -255,8 +264,14 @@ RT_D Ids chunk_ids(const Params& P, uint32_t chunk) {
     return r;
   }
   r.lpix = chunk_pixel(P, chunk, sub);
+#ifdef RT_ABLATE_REVERSED  // timing ablation only (wrong images): the rank's pixels traced in reverse order
+  const uint32_t lrev = (uint32_t)P.npix - 1u - r.lpix;
+  uint32_t row_l = fdiv(lrev, P.fd_width);
+  r.col = lrev - row_l * (uint32_t)P.width;
+#else
   uint32_t row_l = fdiv(r.lpix, P.fd_width);
   r.col = r.lpix - row_l * (uint32_t)P.width;
+#endif
   r.row = row_l * (uint32_t)P.nranks + (uint32_t)P.rank;
   r.gpix = r.row * (uint32_t)P.width + r.col;
   const cst_params* kp = kparams();

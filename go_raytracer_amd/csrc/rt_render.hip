@@ -154,7 +154,12 @@ __global__ __launch_bounds__(256) void k_resolve(Params P, float* out, double sc
   // sample block sub (chunk_pixel), summed mod 2^64 like the atomics they replace
   unsigned long long cs[3] = {0ull, 0ull, 0ull};
   if (P.csum) {
-    const uint32_t gpix = P.fd_gpix.d, q = fdiv(lp, P.fd_gpix), r = lp - q * gpix;
+    const uint32_t gpix = P.fd_gpix.d, g = fdiv(lp, P.fd_gpix), r = lp - g * gpix;
+#ifdef RT_SWEEP_ORDER
+    const uint32_t q = (g ^ P.gflip) + P.gbase;  // the group's sweep position (an involution)
+#else
+    const uint32_t q = g;
+#endif
     for (int ph = 0; ph < 2; ++ph) {  // the first phase's chunks, then the tail's (if any)
       const uint32_t gch = ph ? P.fd_gchunks2.d : P.fd_gchunks.d;
       const uint32_t cpp = ph && P.S1 >= P.ss ? 0u : gch / gpix;
@@ -1241,6 +1246,7 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   p.n_chunks = n_chunks;
   p.P = P;
   p.ss = ss;
+  uint32_t g_ng = 1u;  // chunk-order groups of this rank
   {
     // chunk order (chunk_pixel): groups of `grows` of this rank's rows, so the paths in
     // flight start from a band of a few rows instead of the whole image (C5 -10 %,
@@ -1254,6 +1260,35 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     p.fd_gpix = make_fastdiv(gpix);
     p.fd_gchunks = make_fastdiv(gpix * cpp1);
     p.fd_gchunks2 = make_fastdiv(std::max<uint32_t>(1u, gpix * cpp2));
+    g_ng = rows / grows;
+  }
+  // The order the sweep takes the row groups in (chunk_pixel, k_resolve; images do not
+  // depend on it): RT_SWEEP = forward (image order, the default) or reverse.  A render's tail
+  // is the paths still in flight when the chunk pool runs dry, so it depends on which rows
+  // the sweep ends on: book2's costly bottom rows (fog, the box ground) end its forward sweep,
+  // and its 2- / 8-GPU shares are 2.3 / 3.2 % faster reversed, while C5 and book1 are 1-6 %
+  // slower (the sky ends their reverse sweep right after the metal dragon / the sphere field,
+  // whose long specular paths are then still in flight); no probe of the rows' costs chose
+  // between them reliably, DESIGN.md §8.  Feature-set kernels only (the record loop maps
+  // chunks in one phase).  The group of sweep position q is (q ^ gflip) + gbase, compiled in
+  // only with -DRT_SWEEP_ORDER: even that form, two kernel-argument words and two VALU ops
+  // per chunk start, measured C4 +0.3 % and C5 +0.5 % in the default order at full size
+  // (profiles/r6_sweep_table_cost_ab.jsonl; a table lookup the same).
+#ifdef RT_SWEEP_ORDER
+  p.gflip = p.gbase = 0u;
+#endif
+  {
+    std::string v;
+    if (tune_str("RT_SWEEP", &v) && v == "reverse") {
+#ifdef RT_SWEEP_ORDER
+      if (mode == RT_MODE_FUSED && ft_set != 0u && g_ng > 1 && npix > 0) {
+        p.gflip = ~0u;  // (q ^ ~0) + ng = ng - 1 - q
+        p.gbase = g_ng;
+      }
+#else
+      return set_error(RT_ERR_UNSUPPORTED, "RT_SWEEP=reverse needs a library built with -DRT_SWEEP_ORDER");
+#endif
+    }
   }
   p.fd_width = make_fastdiv(W);
   p.fd_s = make_fastdiv((uint32_t)cd.spp_sqrt);

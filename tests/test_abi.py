@@ -150,13 +150,13 @@ def test_tuning_is_explicit_and_reported(rt, tune):
     ("RT_STEP_BUDGET", "0"), ("RT_STEP_BUDGET", "-3"), ("RT_STEP_BUDGET", "abc"),
     ("RT_STEP_BUDGET", "5x"), ("RT_STEP_BUDGET", ""), ("RT_SHADE_MIN", "0"), ("RT_TAIL_K", "0"),
     ("RT_CHUNK_NEED", "1e3"), ("RT_PARTS_LOG2", "7"), ("RT_BVH_CT", "nan"), ("RT_QBVH", "2"),
-    ("RT_BVH_BUILDER", "gpu"), ("RT_GRAB_MIN", "99999999999999999999"),
+    ("RT_BVH_BUILDER", "gpu"), ("RT_GRAB_MIN", "99999999999999999999"), ("RT_SWEEP", "backwards"),
 ])
 def test_tune_set_refuses_bad_values(rt, tune, name, value):
     """a scheduling knob out of range (a step budget of 0 would leave every traversal
     without steps and the fused loop spinning) is refused with RT_ERR_INVALID, before any render,
     and the knob keeps its previous value."""
-    tune(name, {"RT_BVH_BUILDER": "host", "RT_BVH_CT": "2.5"}.get(name, "1"))
+    tune(name, {"RT_BVH_BUILDER": "host", "RT_BVH_CT": "2.5", "RT_SWEEP": "reverse"}.get(name, "1"))
     before = rt.tune_get(name)
     with pytest.raises(rt.RtError, match="rt_tune_set"):
         rt.tune(name, value)

@@ -84,6 +84,30 @@ def test_drain_split_is_bitwise(rt, gpu, name, nranks, tune):
             assert st["segments"] == st0["segments"], (m, K)
 
 
+@pytest.mark.parametrize("name,width,nranks", [("book1", 96, 1), ("book2", 128, 2),
+                                                ("cornell_smoke", 96, 3), ("cornell", 64, 1)])
+def test_sweep_order_reverse(rt, gpu, name, width, nranks, tune):
+    """The reverse chunk sweep (RT_SWEEP=reverse; rt_path.h chunk_pixel's (q ^ gflip) + gbase,
+    k_resolve's inverse) is an opt-in build, -DRT_SWEEP_ORDER (DESIGN.md §8 "Sweep order": it
+    cost C4/C5 0.3-0.5 % compiled in).  The default library refuses the knob at render time
+    with RT_ERR_UNSUPPORTED instead of ignoring it; a -DRT_SWEEP_ORDER library
+    (RT_AMD_LIB=...) moves work only, so its image and segment count are the forward sweep's,
+    for the whole image and a row share (the record loop, cornell, keeps its one-phase order;
+    tools/order_ab.py measured the same on the full-size configs, bitwise_same)."""
+    t, cam, w, l = _scene(rt, name, width, 32)
+    with rt.Scene(t, w, l) as sc:
+        tune("RT_SWEEP", "forward")
+        ref, st0 = sc.render(cam, seed=3, rank=nranks - 1, nranks=nranks)
+        tune("RT_SWEEP", "reverse")
+        try:
+            img, st = sc.render(cam, seed=3, rank=nranks - 1, nranks=nranks)
+        except rt.RtError as e:
+            assert "RT_SWEEP_ORDER" in str(e)
+            return
+        assert np.array_equal(img, ref, equal_nan=True)
+        assert st["segments"] == st0["segments"]
+
+
 def test_big_spheres_outside_the_bvh_same_image(rt, gpu, tune):
     """Spheres of radius >= kBigSphereR are tested before the BVH (trav_init) instead of as
     BVH leaves: the same fp64 test on the same record, so the same closest hits.  book1's

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""Wave timeline of the fused kernel (dev tool): renders C2 shares with
-RT_WAVE_TIMES set and summarises when waves finish relative to the kernel span.
-usage: python3 tools/wave_timeline.py [nranks ...]"""
+"""Wave timeline of the fused kernel (dev tool): renders C2 shares (or SCENE=name WIDTH=w
+SPP=s) with RT_WAVE_TIMES set and summarises when waves finish relative to the kernel span.
+usage: [SCENE=model WIDTH=1920 SPP=1024] python3 tools/wave_timeline.py [nranks ...]"""
 import json
 import os
 import sys
@@ -12,8 +12,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import go_raytracer_amd as rt  # noqa: E402
 rt.tune_from_env()  # dev tool: RT_* knobs from the environment (rt_tune_set)
 
-t, cam, w, l = rt.demo_scene("cornell")
-cam.Width, cam.SamplesPerPixel = 800, 1024
+SCENE = os.environ.get("SCENE", "cornell")
+t, cam, w, l = rt.demo_scene(SCENE)
+cam.Width = int(os.environ.get("WIDTH", "800"))
+cam.SamplesPerPixel = int(os.environ.get("SPP", "1024"))
 path = "/tmp/wave_times.bin"
 with rt.Scene(t, w, l) as sc:
     for n in [int(x) for x in sys.argv[1:]] or [1, 8]:
@@ -28,7 +30,7 @@ with rt.Scene(t, w, l) as sc:
         span = end.max()
         q = lambda x, p: float(np.percentile(x, p))  # noqa: E731
         print(json.dumps({
-            "nranks": n, "kernel_ms": round(st["ms_fused"], 3), "waves": len(a),
+            "scene": SCENE, "nranks": n, "kernel_ms": round(st["ms_fused"], 3), "waves": len(a),
             "span_us": round(span, 1), "start_p50_us": round(q(start, 50), 1),
             "start_max_us": round(start.max(), 1),
             "end_p1_us": round(q(end, 1), 1), "end_p10_us": round(q(end, 10), 1),
