@@ -164,6 +164,9 @@ __global__ __launch_bounds__(256) void k_resolve(Params P, float* out, double sc
       const uint32_t gch = ph ? P.fd_gchunks2.d : P.fd_gchunks.d;
       const uint32_t cpp = ph && P.S1 >= P.ss ? 0u : gch / gpix;
       const unsigned long long* rec = P.csum + 4 * ((ph ? (size_t)P.n1 : 0) + (size_t)q * gch + r);
+      // unrolled: eight records' loads in flight per thread before the adds wait (one at a
+      // time, the 655 MB of C2's records were read at ~3.5 TB/s)
+#pragma unroll 8
       for (uint32_t sb = 0; sb < cpp; ++sb, rec += 4 * (size_t)gpix) {
         cs[0] += rec[0];
         cs[1] += rec[1];
