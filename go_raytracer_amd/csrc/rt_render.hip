@@ -1075,7 +1075,8 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     if (o.path_slots > 0) fused_blocks = std::max(1, std::min(fused_blocks, (o.path_slots + 255) / 256));
     P = (uint32_t)fused_blocks * 256u;
   }
-  // Samples per chunk.  Fused: the largest K in {32, 16, 8} that still gives
+  // Samples per chunk.  Fused: the largest K in {32, 16, 8} (64 for C2's record loop, below)
+  // that still gives
   // every lane >= 12 chunks (tree in LDS) or >= 100 (tree through L1/L2, whose
   // per-pixel cost varies more), so the last chunks do not leave most lanes idle.
   // Round 4 (partitioned counters, chunk sums as plain stores): C2's 2-, 4- and 8-GPU
@@ -1097,11 +1098,21 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     const uint64_t work = (uint64_t)npix * ss,
                    need = (uint64_t)std::max(1, env_int("RT_CHUNK_NEED", need_dflt)) * P;
     K = f_lds ? 8u : 4u;  // the smallest: C3's 8-GPU share 6 % faster at 4 than 8 (C2's ±1 %)
-    for (uint32_t k : {32u, 16u, 8u})
-      if (work / k >= need) {
-        K = k;
-        break;
-      }
+    // Round 6: the lean record-loop kernel (C2) also takes K = 64 at the same bar (half as
+    // many chunk starts and records; k_resolve reads half the bytes): C2 28.44 -> 27.81 ms
+    // on the whole image, its 2-GPU share -0.6 %; its 4-GPU share, 6.5 chunks per lane at 64,
+    // keeps 32 (7.56-7.65 against 7.81-7.83 ms at 64, profiles/r6_chunk64_share_ab.jsonl),
+    // the 8-GPU share 16 (64: 4.62, 32: 4.39 ms against 4.03), and the tree kernels 32 (64:
+    // book1 +4 %, C5 +1.9 %, book2 +0.5 %; profiles/r6_chunk64_probe.jsonl)
+    if (tree == 0 && ft_set == 0u && work / 64u >= need) {
+      K = 64u;
+    } else {
+      for (uint32_t k : {32u, 16u, 8u})
+        if (work / k >= need) {
+          K = k;
+          break;
+        }
+    }
   }
   K = std::max<uint32_t>(1u, std::min<uint32_t>(std::min(K, ss), 4096u));
   // Tail phase (fused, default chunk sizes): the last ~1/RT_TAIL_FRAC of every pixel's
