@@ -1094,7 +1094,12 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     // (the mesh set asks 200: the 1M-triangle mesh's 2- / 4- / 8-GPU shares -0.6 / -1.6 /
     // -2.3 % with K halved, its whole image unchanged at K = 32; book1 and book2 gained
     // nothing from it, profiles/r5_model_chunk_share_ab.jsonl, r5_chunk_need200_ab.jsonl)
-    const int need_dflt = f_lds ? 12 : ft_set == (FT_SPHERE | FT_TRI | FT_METAL) ? 200 : 100;
+    // Round 6: book1's set asks 50 and may take K = 24.  Its bar of 100 had been met at K = 16
+    // with 4 waves per SIMD; at 5 (round 5) the lanes outnumber it and the rule fell to K = 8:
+    // the whole C3 image 72.2 ms at 8, 71.2 at 16, 70.6 at 24, 71.8 at 32; its 2- and 8-GPU
+    // shares still get 8 and 4 (profiles/r6_chunk_sweep.jsonl)
+    const bool book1_set = ft_set == (FT_SPHERE | FT_TRI | FT_METAL | FT_DIEL | FT_CHECKER);
+    const int need_dflt = f_lds ? 12 : ft_set == (FT_SPHERE | FT_TRI | FT_METAL) ? 200 : book1_set ? 50 : 100;
     const uint64_t work = (uint64_t)npix * ss,
                    need = (uint64_t)std::max(1, env_int("RT_CHUNK_NEED", need_dflt)) * P;
     K = f_lds ? 8u : 4u;  // the smallest: C3's 8-GPU share 6 % faster at 4 than 8 (C2's ±1 %)
@@ -1107,8 +1112,8 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
     if (tree == 0 && ft_set == 0u && work / 64u >= need) {
       K = 64u;
     } else {
-      for (uint32_t k : {32u, 16u, 8u})
-        if (work / k >= need) {
+      for (uint32_t k : {32u, 24u, 16u, 8u})
+        if ((k != 24u || book1_set) && work / k >= need) {
           K = k;
           break;
         }
@@ -1334,7 +1339,9 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   // 5.22 with 128; profiles/r4_share_probe_grab_v1.jsonl, r4_grab_ab.jsonl), while the
   // scenes that traverse a tree through L1/L2 keep 128 (32 measured C3 +3.7 %, C4 +2.2 %,
   // C5 +2 %: their waves refill more often and spread over more of the image)
-  p.grab_min = (uint32_t)std::max(1, env_int("RT_GRAB_MIN", f_lds ? 32 : K <= 8u ? 256 : 128));
+  // (round 6: 16 for C2's 64-sample chunks, -0.4 % against 32, 64 +1 %, 128 +4 %,
+  // profiles/r6_chunk_sweep.jsonl)
+  p.grab_min = (uint32_t)std::max(1, env_int("RT_GRAB_MIN", f_lds ? (K >= 64u ? 16 : 32) : K <= 8u ? 256 : 128));
   {  // drain splitting (k_fused's record-loop kernel): share when >= split_min samples are left
     const int sm = env_int("RT_SPLIT_MIN", 1);
     p.split_min = sm > 0 ? (uint32_t)sm : 0xFFFFFFFFu;  // 0: off (no lane has that many)
