@@ -1329,7 +1329,10 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   // profiles/r5_c4_c5_knobs_full.jsonl)
   // (clamped where read, as every scheduling knob: a round without a traversal step would
   // never finish a traversal)
-  p.step_budget = std::max(1, env_int("RT_STEP_BUDGET", f_lds ? (1 << 30) : big_tree ? (long_shade ? 7 : 5) : 10));
+  // (round 6, with the mesh set's 256-chunk batches: 4 steps -0.5 % on C5's whole image, -0.4 /
+  // -0.6 % on its 2- / 8-GPU shares against 5; 3 as 4 except the 8-GPU share, 2 +1.5 %; the
+  // ready-lane bar 24 as 32, 16 +2.5 %, 40 +2 %; profiles/r6_c5_sched_sweep.jsonl)
+  p.step_budget = std::max(1, env_int("RT_STEP_BUDGET", f_lds ? (1 << 30) : big_tree ? (long_shade ? 7 : 4) : 10));
   p.shade_min = (uint32_t)std::max(1, env_int("RT_SHADE_MIN", f_lds ? 1 : long_shade ? 40 : big_tree ? 32 : 1));
   // chunks per refill of a wave's batch (one returning atomic on the chunk
   // counter each): C2 grab sweep (profiles/r1_grab_sweep.jsonl) 64 -> 128:
