@@ -1342,13 +1342,14 @@ static int render_impl(rt_scene* scene, const rt_camera* cam, const rt_render_op
   // 5.22 with 128; profiles/r4_share_probe_grab_v1.jsonl, r4_grab_ab.jsonl), while the
   // scenes that traverse a tree through L1/L2 keep 128 (32 measured C3 +3.7 %, C4 +2.2 %,
   // C5 +2 %: their waves refill more often and spread over more of the image)
-  // (round 6: 16 for C2's 64-sample chunks, -0.4 % against 32, 64 +1 %, 128 +4 %,
-  // profiles/r6_chunk_sweep.jsonl)
+  // (round 6: 16 for C2's record loop at any K: its whole image at K = 64 -0.4 % against 32
+  // (64 +1 %, 128 +4 %), its 2- / 4-GPU shares -0.9 / -1.3 %, the 8-GPU share ±0;
+  // profiles/r6_chunk_sweep.jsonl, r6_grab_sweep_c2_shares.jsonl)
   // (round 6: 256 for the mesh set at any K: C5 -1.0 % on the whole image, -0.5 % on its 2-GPU
   // share; 512 ±0, 1024 +5 %; book2 keeps 128: -0.4 % whole but +0.4 % on its 2-GPU share, and
   // book1 128: 64 +0.7 %, 256 +2 %; profiles/r6_grab_sweep.jsonl)
   const bool mesh_set = ft_set == (FT_SPHERE | FT_TRI | FT_METAL);
-  p.grab_min = (uint32_t)std::max(1, env_int("RT_GRAB_MIN", f_lds ? (K >= 64u ? 16 : 32) : (K <= 8u || mesh_set) ? 256 : 128));
+  p.grab_min = (uint32_t)std::max(1, env_int("RT_GRAB_MIN", f_lds ? (tree == 0 && ft_set == 0u ? 16 : 32) : (K <= 8u || mesh_set) ? 256 : 128));
   {  // drain splitting (k_fused's record-loop kernel): share when >= split_min samples are left
     const int sm = env_int("RT_SPLIT_MIN", 1);
     p.split_min = sm > 0 ? (uint32_t)sm : 0xFFFFFFFFu;  // 0: off (no lane has that many)
